@@ -1,0 +1,204 @@
+/*
+ * mi_cls.h -- thin C ABI between the (C) ODP host side and the hand-written
+ * gfx950 HIP kernels of the MI355X packet parse + PMR classify path.
+ *
+ * This ABI is the device-side, batch form of the two per-packet internal
+ * calls that every linux-generic pktio driver's .recv op makes
+ * (pktio_if_ops_t.recv, platform/linux-generic/include/odp_packet_io_internal.h:222;
+ * loop driver: platform/linux-generic/pktio/loop.c:253-384):
+ *
+ *   _odp_packet_parse_common()   platform/linux-generic/include/odp_parse_internal.h:80-112
+ *   _odp_cls_classify_packet()   platform/linux-generic/odp_classification.c:1742-1771
+ *
+ * One call of mi_cls_classify() replaces the per-packet pair for a whole
+ * batch of contiguous packets already resident in device memory.  All
+ * pointers are plain device pointers; the caller owns every buffer.  Every
+ * entry point returns 0 on success or a negative errno.
+ *
+ * Threading: one mi_cls_ctx_t per GPU; calls on one context are
+ * serialised by the caller (mirrors the reference's lock-free data plane
+ * reading rule tables that the control plane snapshots, odp_classification.c:1373).
+ */
+#ifndef MI_CLS_H_
+#define MI_CLS_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------------
+ * Per-packet result record (16 bytes, written by the kernel).
+ * Mirrors the packet-header fields the reference fills in
+ * (odp_packet_hdr_t.p / .cos / .dst_queue / .cls_mark,
+ *  platform/linux-generic/include/odp_packet_internal.h:55-70,112,116,139):
+ *   in_flags  - low 32 bits of packet_parser_t.input_flags.all (bits >= 32
+ *               are never set by this path; layout: packet_inline_types.h:60-107)
+ *   err       - flags.all.error, 7 bits: snap_len, ip, l3_chksum, tcp, udp,
+ *               sctp, l4_chksum (packet_inline_types.h:152-165)
+ *   outcome   - MI_CLS_OUT_* below (the 0 / 1 / -1 return protocol of
+ *               _odp_packet_parse_common and _odp_cls_classify_packet)
+ *   cos       - CoS index (cos_t.index, the slot number), 0xFF when none
+ *   hops      - number of PMR matches on the CoS descent (diagnostic)
+ *   queue     - queue slot inside the CoS: 0 for a single-queue CoS, the
+ *               Toeplitz hash slot for a hash-queue CoS (get_dest_queue,
+ *               odp_classification.c:395-405); the host maps (cos, slot) to
+ *               the odp_queue_t handle
+ *   mark      - hdr->cls_mark (valid when in_flags bit 0, cls_mark, is set)
+ *   l3/l4     - packet_parser_t.l3_offset / l4_offset (0xFFFF = invalid);
+ *               l2_offset is always 0 on this path and is not stored.
+ * ---------------------------------------------------------------------- */
+typedef struct mi_cls_result {
+	uint32_t in_flags;
+	uint8_t  err;
+	uint8_t  outcome;
+	uint8_t  cos;
+	uint8_t  hops;
+	uint16_t queue;
+	uint16_t mark;
+	uint16_t l3_offset;
+	uint16_t l4_offset;
+} mi_cls_result_t;
+
+enum {
+	MI_CLS_OUT_ENQ        = 0, /* classify returned 0: enqueue to (cos, queue)        */
+	MI_CLS_OUT_COS_DROP   = 1, /* classify returned 1: CoS action DROP (silent drop)   */
+	MI_CLS_OUT_DISCARD    = 2, /* classify returned -1: no CoS (in_discards++)         */
+	MI_CLS_OUT_PARSE_DROP = 3, /* parse returned -1: truncated L4 header (in_errors++) */
+	MI_CLS_OUT_LOOP       = 4  /* CoS graph cycle: the reference never returns here    */
+};
+
+/* ------------------------------------------------------------------------
+ * Compiled rule table ("snapshot" of the control-plane CoS/PMR tables,
+ * platform/linux-generic/include/odp_classification_datamodel.h:126-206).
+ * One contiguous, position-independent little-endian blob of 32-bit words:
+ *   mi_tbl_hdr_t | mi_cos_t[num_cos] | mi_rule_t[num_rules] | mi_term_t[num_terms]
+ * Rules of a CoS are stored contiguously in cos->pmr[] order (the order the
+ * reference scans them, match_pmr_cos, odp_classification.c:1631), with
+ * entries whose linked CoS is invalid already removed (:1635-1636).
+ * ---------------------------------------------------------------------- */
+#define MI_CLS_TBL_MAGIC   0x534C434Du /* "MCLS" */
+#define MI_CLS_TBL_VERSION 1u
+
+typedef struct mi_tbl_hdr {
+	uint32_t magic;
+	uint32_t version;
+	uint32_t total_bytes;
+	uint32_t num_cos;       /* CoS slots described (= max slot used + 1)          */
+	uint32_t num_rules;
+	uint32_t num_terms;
+	int32_t  default_cos;   /* slot, -1 = none (classifier_t.default_cos)         */
+	int32_t  error_cos;     /* slot, -1 = none (classifier_t.error_cos)           */
+	uint32_t default_valid; /* default_cos->valid at snapshot time (:1712)        */
+	uint32_t used_kinds;    /* bit per MI_K_* present anywhere in the table       */
+	uint32_t max_hops;      /* descent bound (cycle guard)                        */
+	uint32_t cos_off;       /* byte offsets of the three arrays from the header   */
+	uint32_t rule_off;
+	uint32_t term_off;
+	uint32_t generation;    /* control-plane generation this snapshot reflects    */
+	uint32_t rsv;
+} mi_tbl_hdr_t;
+
+typedef struct mi_cos {
+	uint32_t rule_begin;
+	uint32_t num_rules;
+	uint8_t  action;        /* 0 enqueue, 1 drop (odp_cos_action_t)              */
+	uint8_t  num_queue;     /* 1..32                                             */
+	uint8_t  hash_proto;    /* cos_t.hash_proto: bit0 ipv4, 1 ipv6, 2 udp, 3 tcp */
+	uint8_t  index;         /* cos_t.index                                       */
+	uint32_t valid;
+} mi_cos_t;
+
+typedef struct mi_rule {
+	uint32_t term_begin;
+	uint16_t num_terms;     /* 0..8; 0 matches everything                       */
+	uint16_t mark;
+	uint32_t dst_cos;       /* linked CoS slot                                  */
+	uint32_t rsv;
+} mi_rule_t;
+
+/* Compiled term kinds (one per verify_pmr_<term>, odp_classification.c:931-1357) */
+enum {
+	MI_K_LEN = 0,      /* frame_len (host order) & mask == value                 */
+	MI_K_ETH0,         /* raw bytes at l2+12, gate eth                           */
+	MI_K_ETHX,         /* raw bytes at l2+16 / +20 (qinq), gate vlan|qinq        */
+	MI_K_VID0,         /* raw tci at l2+14 & be16(0x0fff), gate eth&vlan         */
+	MI_K_VIDX,         /* raw tci at l2+14 / +18, & be16(0x0fff), gate vlan|qinq */
+	MI_K_PCP0,         /* tci>>13 (host order), gate eth&vlan                    */
+	MI_K_DMAC,         /* 6 raw bytes at l2, gate eth                            */
+	MI_K_PROTO,        /* ipv4 proto / ipv6 fixed next_hdr, gate ipv4|ipv6       */
+	MI_K_DSCP,         /* tos>>2 / (vtf&0x0fc00000)>>22, gate ipv4|ipv6          */
+	MI_K_UDP_DPORT,
+	MI_K_TCP_DPORT,
+	MI_K_UDP_SPORT,
+	MI_K_TCP_SPORT,
+	MI_K_SIP,
+	MI_K_DIP,
+	MI_K_SIP6,
+	MI_K_DIP6,
+	MI_K_SPI,          /* l4+4 (AH) / l4+0 (ESP)                                 */
+	MI_K_NEVER,        /* LD_VNI: accepted at create, never matches (:1250)      */
+	MI_K_CUSTOM_FRAME, /* bytes at offset, gate len > offset+size                */
+	MI_K_CUSTOM_L3,    /* bytes at l3+offset, gate l2 & l3 valid & len > ...     */
+	MI_K_ALWAYS,       /* INNER_HDR_OFF: always passes (:1504)                   */
+	MI_K_COUNT
+};
+
+typedef struct mi_term {
+	uint8_t  kind;          /* MI_K_*                                            */
+	uint8_t  size;          /* val_sz                                            */
+	uint16_t rsv0;
+	uint32_t offset;        /* custom offset                                     */
+	uint32_t rsv1[2];
+	uint32_t mask[4];       /* little-endian packing of the mask bytes           */
+	uint32_t value[4];      /* pre-masked value bytes (pmr_create_term, :757)    */
+} mi_term_t;
+
+/* ------------------------------------------------------------------------
+ * Context and entry points
+ * ---------------------------------------------------------------------- */
+typedef struct mi_cls_ctx mi_cls_ctx_t;
+
+/* Number of visible HIP devices (>= 0), or a negative errno. */
+int mi_cls_device_count(void);
+
+/* Create a classification context bound to HIP device `device`. */
+int mi_cls_ctx_create(int device, mi_cls_ctx_t **ctx);
+int mi_cls_ctx_destroy(mi_cls_ctx_t *ctx);
+
+/* Upload a compiled rule table (host memory, mi_tbl_hdr_t blob) to the
+ * context's device copy, stream-ordered on `stream` (hipStream_t, NULL =
+ * default stream).  Validates the blob; -EINVAL on a malformed table. */
+int mi_cls_rules_load(mi_cls_ctx_t *ctx, const void *tbl, size_t bytes, void *stream);
+
+/* Parse + classify n packets.
+ *   pkts_dev  packed packet bytes; each packet starts at pkts_dev + off_dev[i]
+ *             (16-byte aligned offsets take the fast staging path; others are
+ *             still correct) and the buffer must be readable up to the next
+ *             16-byte boundary after each packet (true of any hipMalloc).
+ *   off_dev   uint32 byte offsets, len_dev uint16 frame lengths (FCS stripped)
+ *   out_dev   n result records
+ * Stream-ordered on `stream`; returns after the launch is enqueued. */
+int mi_cls_classify(mi_cls_ctx_t *ctx, const uint8_t *pkts_dev, const uint32_t *off_dev,
+		    const uint16_t *len_dev, uint32_t n, mi_cls_result_t *out_dev,
+		    void *stream);
+
+/* Per-CoS packet counters with the reference's per-hop counting rule
+ * (odp_classification.c:1646-1647, 1721-1723): when enabled, each
+ * mi_cls_classify() adds into a device array of num_cos uint64 counters
+ * for CoS slots whose stats are enabled (stats_mask bit per slot, up to 256).
+ * mi_cls_stats_read copies the counters to host memory (synchronous). */
+int mi_cls_stats_enable(mi_cls_ctx_t *ctx, const uint32_t stats_mask[8]);
+int mi_cls_stats_read(mi_cls_ctx_t *ctx, uint64_t *host_counters, uint32_t num);
+int mi_cls_stats_reset(mi_cls_ctx_t *ctx);
+
+/* Last error string for the context (static storage, never NULL). */
+const char *mi_cls_strerror(int err);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MI_CLS_H_ */

@@ -1,0 +1,358 @@
+/*
+ * odp_cls_api.h -- the ODP classification API surface served by the MI355X
+ * build (libodp_cls.so).  Names, argument meaning, handle conventions and
+ * error behaviour follow the reference API:
+ *
+ *   include/odp/api/spec/classification.h        (types :55-770, functions :779-1158)
+ *   include/odp/api/spec/packet_io.h:695-747     (pktio-side CoS setters)
+ *   platform/linux-generic/odp_classification.c  (linux-generic semantics)
+ *
+ * Handles are index+1 and the INVALID handle is 0 (odp_classification.c:60-78).
+ * Creation returns INVALID on failure; *_multi returns the number created or -1
+ * when the first fails; destroy returns 0 / -1.  The library owns the rule
+ * tables; value/mask buffers are copied at create time.
+ *
+ * Queue and pool handles are stored and returned, never dereferenced: the
+ * classifier only needs them as opaque identities (the queue / pool
+ * subsystems of ODP are outside this build's scope).
+ */
+#ifndef ODP_AMD_CLS_API_H_
+#define ODP_AMD_CLS_API_H_
+
+#include <stdbool.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef bool odp_bool_t;
+
+/* opaque pointer-sized handles, 0 == INVALID (abi-default headers) */
+typedef struct _odp_abi_cos_t   *odp_cos_t;
+typedef struct _odp_abi_pmr_t   *odp_pmr_t;
+typedef struct _odp_abi_queue_t *odp_queue_t;
+typedef struct _odp_abi_pool_t  *odp_pool_t;
+typedef struct _odp_abi_pktio_t *odp_pktio_t;
+typedef struct _odp_abi_packet_t *odp_packet_t;
+
+#define ODP_COS_INVALID   ((odp_cos_t)0)
+#define ODP_PMR_INVALID   ((odp_pmr_t)0)
+#define ODP_QUEUE_INVALID ((odp_queue_t)0)
+#define ODP_POOL_INVALID  ((odp_pool_t)0)
+#define ODP_PKTIO_INVALID ((odp_pktio_t)0)
+#define ODP_COS_NAME_LEN  32
+
+typedef enum { ODP_SUPPORT_NO = 0, ODP_SUPPORT_YES, ODP_SUPPORT_PREFERRED } odp_support_t;
+
+/* classification.h:55-137 -- enum order is ABI */
+typedef enum {
+	ODP_PMR_LEN,
+	ODP_PMR_ETHTYPE_0,
+	ODP_PMR_ETHTYPE_X,
+	ODP_PMR_VLAN_ID_0,
+	ODP_PMR_VLAN_ID_X,
+	ODP_PMR_VLAN_PCP_0,
+	ODP_PMR_DMAC,
+	ODP_PMR_IPPROTO,
+	ODP_PMR_IP_DSCP,
+	ODP_PMR_UDP_DPORT,
+	ODP_PMR_TCP_DPORT,
+	ODP_PMR_UDP_SPORT,
+	ODP_PMR_TCP_SPORT,
+	ODP_PMR_SIP_ADDR,
+	ODP_PMR_DIP_ADDR,
+	ODP_PMR_SIP6_ADDR,
+	ODP_PMR_DIP6_ADDR,
+	ODP_PMR_IPSEC_SPI,
+	ODP_PMR_LD_VNI,
+	ODP_PMR_CUSTOM_FRAME,
+	ODP_PMR_CUSTOM_L3,
+	ODP_PMR_IGMP_GRP_ADDR,
+	ODP_PMR_ICMP_ID,
+	ODP_PMR_ICMP_TYPE,
+	ODP_PMR_ICMP_CODE,
+	ODP_PMR_SCTP_SPORT,
+	ODP_PMR_SCTP_DPORT,
+	ODP_PMR_GTPV1_TEID,
+	ODP_PMR_INNER_HDR_OFF = 32
+} odp_cls_pmr_term_t;
+
+typedef union odp_cls_pmr_terms_t {
+	struct {
+		uint64_t len:1;
+		uint64_t ethtype_0:1;
+		uint64_t ethtype_x:1;
+		uint64_t vlan_id_0:1;
+		uint64_t vlan_id_x:1;
+		uint64_t vlan_pcp_0:1;
+		uint64_t dmac:1;
+		uint64_t ip_proto:1;
+		uint64_t ip_dscp:1;
+		uint64_t udp_dport:1;
+		uint64_t tcp_dport:1;
+		uint64_t udp_sport:1;
+		uint64_t tcp_sport:1;
+		uint64_t sip_addr:1;
+		uint64_t dip_addr:1;
+		uint64_t sip6_addr:1;
+		uint64_t dip6_addr:1;
+		uint64_t ipsec_spi:1;
+		uint64_t ld_vni:1;
+		uint64_t custom_frame:1;
+		uint64_t custom_l3:1;
+		uint64_t igmp_grp_addr:1;
+		uint64_t icmp_id:1;
+		uint64_t icmp_type:1;
+		uint64_t icmp_code:1;
+		uint64_t sctp_sport:1;
+		uint64_t sctp_dport:1;
+		uint64_t gtpv1_teid:1;
+	} bit;
+	uint64_t all_bits;
+} odp_cls_pmr_terms_t;
+
+/* classification.h:278-321 */
+typedef struct odp_pmr_param_t {
+	odp_cls_pmr_term_t term;
+	odp_bool_t range_term;
+	union {
+		struct {
+			const void *value;
+			const void *mask;
+		} match;
+		struct {
+			const void *val_start;
+			const void *val_end;
+		} range;
+	};
+	uint32_t val_sz;
+	uint32_t offset;
+} odp_pmr_param_t;
+
+typedef struct odp_pmr_create_opt_t {
+	odp_pmr_param_t *terms;
+	int num_terms;
+	uint64_t mark;
+	uint32_t priority;
+} odp_pmr_create_opt_t;
+
+/* packet_io_types.h:124-146 */
+typedef union odp_pktin_hash_proto_t {
+	struct {
+		uint32_t ipv4_udp : 1;
+		uint32_t ipv4_tcp : 1;
+		uint32_t ipv4     : 1;
+		uint32_t ipv6_udp : 1;
+		uint32_t ipv6_tcp : 1;
+		uint32_t ipv6     : 1;
+	} proto;
+	uint32_t all_bits;
+} odp_pktin_hash_proto_t;
+
+typedef struct odp_threshold_types_t {
+	uint8_t all_bits;
+} odp_threshold_types_t;
+
+typedef struct odp_cls_cos_stats_t {
+	uint64_t octets;
+	uint64_t packets;
+	uint64_t discards;
+	uint64_t errors;
+} odp_cls_cos_stats_t;
+
+typedef struct odp_cls_queue_stats_t {
+	uint64_t octets;
+	uint64_t packets;
+	uint64_t discards;
+	uint64_t errors;
+} odp_cls_queue_stats_t;
+
+typedef struct odp_cls_stats_capability_t {
+	struct {
+		union {
+			struct {
+				uint64_t octets   : 1;
+				uint64_t packets  : 1;
+				uint64_t discards : 1;
+				uint64_t errors   : 1;
+			} counter;
+			uint64_t all_counters;
+		};
+	} cos;
+	struct {
+		union {
+			struct {
+				uint64_t octets   : 1;
+				uint64_t packets  : 1;
+				uint64_t discards : 1;
+				uint64_t errors   : 1;
+			} counter;
+			uint64_t all_counters;
+		};
+	} queue;
+} odp_cls_stats_capability_t;
+
+typedef struct odp_cls_capability_t {
+	odp_cls_pmr_terms_t supported_terms;
+	uint32_t max_pmr;
+	uint32_t max_pmr_per_cos;
+	uint32_t max_terms_per_pmr;
+	uint32_t max_pmr_priority;
+	uint32_t max_cos;
+	uint32_t max_cos_stats;
+	uint32_t max_hash_queues;
+	odp_pktin_hash_proto_t hash_protocols;
+	odp_bool_t pmr_range_supported;
+	odp_support_t random_early_detection;
+	odp_threshold_types_t threshold_red;
+	odp_support_t back_pressure;
+	odp_threshold_types_t threshold_bp;
+	uint64_t max_mark;
+	odp_cls_stats_capability_t stats;
+} odp_cls_capability_t;
+
+typedef enum {
+	ODP_COS_ACTION_ENQUEUE,
+	ODP_COS_ACTION_DROP,
+} odp_cos_action_t;
+
+/* Parameters of the implementation-created hash queues.  The queue subsystem
+ * is not part of this build; the struct is kept for source compatibility and
+ * passed through unchanged. */
+typedef struct odp_queue_param_t {
+	int type;
+	int num_aggr;
+	uint8_t opaque[64];
+} odp_queue_param_t;
+
+typedef struct odp_pktin_vector_config_t {
+	odp_bool_t enable;
+	odp_pool_t pool;
+	uint64_t max_tmo_ns;
+	uint32_t max_size;
+} odp_pktin_vector_config_t;
+
+typedef enum {
+	ODP_AEP_TYPE_NONE = 0,
+	ODP_AEP_TYPE_IPV4_FRAG,
+	ODP_AEP_TYPE_IPV6_FRAG,
+	ODP_AEP_TYPE_CUSTOM
+} odp_aggr_enq_profile_type_t;
+
+typedef struct odp_aggr_enq_profile_t {
+	odp_aggr_enq_profile_type_t type;
+	uintptr_t param;
+} odp_aggr_enq_profile_t;
+
+typedef struct odp_red_param_t {
+	odp_bool_t enable;
+	uint64_t threshold;
+} odp_red_param_t;
+
+typedef struct odp_bp_param_t {
+	odp_bool_t enable;
+	uint64_t threshold;
+	uint8_t pfc_level;
+} odp_bp_param_t;
+
+/* classification.h:647-770 -- queue and {queue_param, hash_proto} share a union */
+typedef struct odp_cls_cos_param {
+	odp_cos_action_t action;
+	odp_bool_t stats_enable;
+	uint32_t num_queue;
+	union {
+		odp_queue_t queue;
+		struct {
+			odp_queue_param_t queue_param;
+			odp_pktin_hash_proto_t hash_proto;
+		};
+	};
+	odp_pool_t pool;
+	odp_red_param_t red;
+	odp_bp_param_t bp;
+	odp_pktin_vector_config_t vector;
+	odp_aggr_enq_profile_t aggr_enq_profile;
+} odp_cls_cos_param_t;
+
+/* ---------------------------------------------------------------- API */
+void odp_cls_cos_param_init(odp_cls_cos_param_t *param);
+int odp_cls_capability(odp_cls_capability_t *capability);
+odp_cos_t odp_cls_cos_create(const char *name, const odp_cls_cos_param_t *param);
+int odp_cls_cos_create_multi(const char *name[], const odp_cls_cos_param_t param[],
+			     odp_cos_t cos[], int num);
+int odp_cos_destroy(odp_cos_t cos);
+int odp_cos_destroy_multi(odp_cos_t cos[], int num);
+int odp_cos_queue_set(odp_cos_t cos, odp_queue_t queue);
+odp_queue_t odp_cos_queue(odp_cos_t cos);
+uint32_t odp_cls_cos_num_queue(odp_cos_t cos);
+uint32_t odp_cls_cos_queues(odp_cos_t cos, odp_queue_t queue[], uint32_t num);
+int odp_cls_cos_stats(odp_cos_t cos, odp_cls_cos_stats_t *stats);
+int odp_cls_queue_stats(odp_cos_t cos, odp_queue_t queue, odp_cls_queue_stats_t *stats);
+void odp_cls_pmr_param_init(odp_pmr_param_t *param);
+void odp_cls_pmr_create_opt_init(odp_pmr_create_opt_t *opt);
+odp_pmr_t odp_cls_pmr_create(const odp_pmr_param_t *terms, int num_terms,
+			     odp_cos_t src_cos, odp_cos_t dst_cos);
+odp_pmr_t odp_cls_pmr_create_opt(const odp_pmr_create_opt_t *opt,
+				 odp_cos_t src_cos, odp_cos_t dst_cos);
+int odp_cls_pmr_create_multi(const odp_pmr_create_opt_t opt[], odp_cos_t src_cos[],
+			     odp_cos_t dst_cos[], odp_pmr_t pmr[], int num);
+int odp_cls_pmr_destroy(odp_pmr_t pmr);
+int odp_cls_pmr_destroy_multi(odp_pmr_t pmr[], int num);
+int odp_cls_cos_pool_set(odp_cos_t cos, odp_pool_t pool_id);
+odp_pool_t odp_cls_cos_pool(odp_cos_t cos);
+uint64_t odp_cos_to_u64(odp_cos_t cos);
+uint64_t odp_pmr_to_u64(odp_pmr_t pmr);
+void odp_cls_print_all(void);
+
+/* packet_io.h:695-747 */
+int odp_pktio_default_cos_set(odp_pktio_t pktio, odp_cos_t default_cos);
+int odp_pktio_error_cos_set(odp_pktio_t pktio, odp_cos_t error_cos);
+int odp_pktio_skip_set(odp_pktio_t pktio, uint32_t offset);
+int odp_pktio_headroom_set(odp_pktio_t pktio, uint32_t headroom);
+
+/* ------------------------------------------------------------------
+ * MI355X build extensions (not in the ODP spec).
+ * ---------------------------------------------------------------- */
+
+/* Table limits.  The stock linux-generic limits are 64 CoS / 256 PMR /
+ * 8 PMR per CoS (odp_classification_datamodel.h:32-40); this build defaults
+ * to the raised limits the BASELINE configs need (255 / 8192 / 4096), with
+ * unchanged lookup semantics.  Must be called before any other cls call. */
+int odp_amd_cls_limits_set(uint32_t max_cos, uint32_t max_pmr, uint32_t max_pmr_per_cos);
+/* Reset all classifier state (tables, pktio bindings); test helper. */
+void odp_amd_cls_reset(void);
+
+/* A classifier-enabled receive endpoint bound to one GPU: the classifier_t
+ * of a pktio entry (odp_classification_datamodel.h:176-181) plus its device
+ * context.  odp_pktio_open() of the ODP runtime layer creates these. */
+odp_pktio_t odp_amd_cls_pktio_create(int gpu);
+int odp_amd_cls_pktio_destroy(odp_pktio_t pktio);
+
+/* Snapshot ("compile") the current tables into the mi_cls.h blob format.
+ * Returns the blob size; writes at most cap bytes into buf (buf may be NULL
+ * to query the size). */
+long odp_amd_cls_compile(odp_pktio_t pktio, void *buf, size_t cap);
+
+/* Receive-path batch classify: parse + classify n packets already resident
+ * in device memory (layout: include/mi_cls.h).  Recompiles and uploads the
+ * rule snapshot when the control plane changed since the last call. */
+int odp_amd_cls_classify(odp_pktio_t pktio, const uint8_t *pkts_dev, const uint32_t *off_dev,
+			 const uint16_t *len_dev, uint32_t n, void *out_dev, void *stream);
+
+/* Map a result record's (cos index, queue slot) to the odp_queue_t handle
+ * (queue_grp_tbl / cos->queue lookup of get_dest_queue, :395-405). */
+odp_queue_t odp_amd_cls_queue_of(uint32_t cos_index, uint32_t queue_slot);
+
+/* Control-plane generation counter (bumped by every table change). */
+uint64_t odp_amd_cls_generation(void);
+
+/* sizeof / offsetof of the ABI structs (binding self-check). */
+size_t odp_amd_cls_abi_size(int which);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ODP_AMD_CLS_API_H_ */

@@ -1,0 +1,274 @@
+"""ctypes binding of libodp_cls.so (include/odp_cls_api.h) and libmi_cls.so.
+
+This is the host-side mirror of the reference's classifier interface
+(include/odp/api/spec/classification.h) used by the tests and bench: the
+same function names, argument meaning and error behaviour (INVALID handle
+= 0 on failure, -1 from destroy, ...).  The compute path is the HIP kernel in
+libmi_cls.so; there is no CPU fallback -- loading fails loudly if the
+native libraries are missing.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import rules as R
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_MI = os.path.join(_HERE, "libmi_cls.so")
+LIB_ODP = os.path.join(_HERE, "libodp_cls.so")
+
+
+class PmrParam(C.Structure):
+    """odp_pmr_param_t (classification.h:278-321)."""
+    _fields_ = [("term", C.c_int), ("range_term", C.c_bool), ("value", C.c_void_p),
+                ("mask", C.c_void_p), ("val_sz", C.c_uint32), ("offset", C.c_uint32)]
+
+
+class PmrCreateOpt(C.Structure):
+    """odp_pmr_create_opt_t."""
+    _fields_ = [("terms", C.POINTER(PmrParam)), ("num_terms", C.c_int), ("mark", C.c_uint64),
+                ("priority", C.c_uint32)]
+
+
+class QueueParam(C.Structure):
+    _fields_ = [("type", C.c_int), ("num_aggr", C.c_int), ("opaque", C.c_uint8 * 64)]
+
+
+class _QP(C.Structure):
+    _fields_ = [("queue_param", QueueParam), ("hash_proto", C.c_uint32)]
+
+
+class _QU(C.Union):
+    _fields_ = [("queue", C.c_void_p), ("qp", _QP)]
+
+
+class RedParam(C.Structure):
+    _fields_ = [("enable", C.c_bool), ("threshold", C.c_uint64)]
+
+
+class BpParam(C.Structure):
+    _fields_ = [("enable", C.c_bool), ("threshold", C.c_uint64), ("pfc_level", C.c_uint8)]
+
+
+class VectorCfg(C.Structure):
+    _fields_ = [("enable", C.c_bool), ("pool", C.c_void_p), ("max_tmo_ns", C.c_uint64),
+                ("max_size", C.c_uint32)]
+
+
+class AggrProfile(C.Structure):
+    _fields_ = [("type", C.c_int), ("param", C.c_void_p)]
+
+
+class CosParam(C.Structure):
+    """odp_cls_cos_param_t (classification.h:647-770)."""
+    _anonymous_ = ("u",)
+    _fields_ = [("action", C.c_int), ("stats_enable", C.c_bool), ("num_queue", C.c_uint32),
+                ("u", _QU), ("pool", C.c_void_p), ("red", RedParam), ("bp", BpParam),
+                ("vector", VectorCfg), ("aggr_enq_profile", AggrProfile)]
+
+
+class CosStats(C.Structure):
+    _fields_ = [("octets", C.c_uint64), ("packets", C.c_uint64), ("discards", C.c_uint64),
+                ("errors", C.c_uint64)]
+
+
+class Capability(C.Structure):
+    _fields_ = [("supported_terms", C.c_uint64), ("max_pmr", C.c_uint32),
+                ("max_pmr_per_cos", C.c_uint32), ("max_terms_per_pmr", C.c_uint32),
+                ("max_pmr_priority", C.c_uint32), ("max_cos", C.c_uint32),
+                ("max_cos_stats", C.c_uint32), ("max_hash_queues", C.c_uint32),
+                ("hash_protocols", C.c_uint32), ("pmr_range_supported", C.c_bool),
+                ("random_early_detection", C.c_int), ("threshold_red", C.c_uint8),
+                ("back_pressure", C.c_int), ("threshold_bp", C.c_uint8),
+                ("max_mark", C.c_uint64), ("stats_cos", C.c_uint64), ("stats_queue", C.c_uint64)]
+
+
+def _load():
+    for p in (LIB_MI, LIB_ODP):
+        if not os.path.exists(p):
+            raise RuntimeError(f"{p} is missing: run __graft_entry__.build() (no CPU fallback)")
+    C.CDLL(LIB_MI, mode=C.RTLD_GLOBAL)
+    lib = C.CDLL(LIB_ODP)
+    vp, u32, i32 = C.c_void_p, C.c_uint32, C.c_int
+    sig = {
+        "odp_cls_cos_param_init": (None, [C.POINTER(CosParam)]),
+        "odp_cls_capability": (i32, [C.POINTER(Capability)]),
+        "odp_cls_cos_create": (vp, [C.c_char_p, C.POINTER(CosParam)]),
+        "odp_cos_destroy": (i32, [vp]),
+        "odp_cos_queue_set": (i32, [vp, vp]),
+        "odp_cos_queue": (vp, [vp]),
+        "odp_cls_cos_num_queue": (u32, [vp]),
+        "odp_cls_cos_queues": (u32, [vp, C.POINTER(vp), u32]),
+        "odp_cls_cos_stats": (i32, [vp, C.POINTER(CosStats)]),
+        "odp_cls_pmr_param_init": (None, [C.POINTER(PmrParam)]),
+        "odp_cls_pmr_create": (vp, [C.POINTER(PmrParam), i32, vp, vp]),
+        "odp_cls_pmr_create_opt": (vp, [C.POINTER(PmrCreateOpt), vp, vp]),
+        "odp_cls_pmr_destroy": (i32, [vp]),
+        "odp_cls_cos_pool_set": (i32, [vp, vp]),
+        "odp_cls_cos_pool": (vp, [vp]),
+        "odp_cos_to_u64": (C.c_uint64, [vp]),
+        "odp_pmr_to_u64": (C.c_uint64, [vp]),
+        "odp_cls_print_all": (None, []),
+        "odp_pktio_default_cos_set": (i32, [vp, vp]),
+        "odp_pktio_error_cos_set": (i32, [vp, vp]),
+        "odp_pktio_skip_set": (i32, [vp, u32]),
+        "odp_pktio_headroom_set": (i32, [vp, u32]),
+        "odp_amd_cls_limits_set": (i32, [u32, u32, u32]),
+        "odp_amd_cls_reset": (None, []),
+        "odp_amd_cls_pktio_create": (vp, [i32]),
+        "odp_amd_cls_pktio_destroy": (i32, [vp]),
+        "odp_amd_cls_compile": (C.c_long, [vp, vp, C.c_size_t]),
+        "odp_amd_cls_classify": (i32, [vp, vp, vp, vp, u32, vp, vp]),
+        "odp_amd_cls_queue_of": (vp, [u32, u32]),
+        "odp_amd_cls_generation": (C.c_uint64, []),
+        "mi_cls_device_count": (i32, []),
+        "mi_cls_ctx_create": (i32, [i32, C.POINTER(vp)]),
+        "mi_cls_ctx_destroy": (i32, [vp]),
+        "mi_cls_rules_load": (i32, [vp, vp, C.c_size_t, vp]),
+        "mi_cls_classify": (i32, [vp, vp, vp, vp, u32, vp, vp]),
+        "mi_cls_strerror": (C.c_char_p, [i32]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    return lib
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        _lib = _load()
+    return _lib
+
+
+def _h(x):
+    return x or 0
+
+
+class Classifier:
+    """One classifier-enabled receive endpoint (pktio) on one GPU, driven
+    through the ODP classification API.  ``apply(program)`` replays a rule
+    program (odp_amd.rules) with odp_cls_* calls."""
+
+    def __init__(self, gpu: int = 0, limits=(255, 8192, 4096)):
+        L = lib()
+        L.odp_amd_cls_reset()
+        if limits is not None:
+            assert L.odp_amd_cls_limits_set(*limits) == 0
+        self.L = L
+        self.pktio = L.odp_amd_cls_pktio_create(gpu)
+        if not self.pktio:
+            raise RuntimeError("odp_amd_cls_pktio_create failed")
+        self.cos = []
+        self.pmr = []
+        self._keep = []
+
+    def close(self):
+        if self.pktio:
+            self.L.odp_amd_cls_pktio_destroy(self.pktio)
+            self.pktio = None
+
+    # -- API passthroughs ------------------------------------------------
+    def cos_create(self, name, action=0, queue=1, num_queue=1, hash_proto=0, stats=0, pool=0):
+        p = CosParam()
+        self.L.odp_cls_cos_param_init(C.byref(p))
+        p.action = action
+        p.num_queue = num_queue
+        p.stats_enable = bool(stats)
+        if num_queue > 1:
+            p.qp.hash_proto = hash_proto
+        else:
+            p.queue = queue
+        p.pool = pool
+        return _h(self.L.odp_cls_cos_create(name.encode() if name else None, C.byref(p)))
+
+    def _terms(self, terms):
+        arr = (PmrParam * max(1, len(terms)))()
+        keep = []
+        for i, (term, value, mask, offset) in enumerate(terms):
+            vb = C.create_string_buffer(bytes(value), max(1, len(value)))
+            mb = C.create_string_buffer(bytes(mask), max(1, len(mask)))
+            keep += [vb, mb]
+            arr[i].term = term
+            arr[i].range_term = False
+            arr[i].value = C.cast(vb, C.c_void_p)
+            arr[i].mask = C.cast(mb, C.c_void_p)
+            arr[i].val_sz = len(value)
+            arr[i].offset = offset
+        return arr, keep
+
+    def pmr_create(self, terms, src, dst, mark=0):
+        arr, keep = self._terms(terms)
+        if mark:
+            o = PmrCreateOpt()
+            o.terms = C.cast(arr, C.POINTER(PmrParam))
+            o.num_terms = len(terms)
+            o.mark = mark
+            o.priority = 0
+            return _h(self.L.odp_cls_pmr_create_opt(C.byref(o), src, dst))
+        return _h(self.L.odp_cls_pmr_create(C.cast(arr, C.POINTER(PmrParam)), len(terms), src, dst))
+
+    def apply(self, prog):
+        """Replay a rule program; returns (cos handles, pmr handles)."""
+        for op in prog:
+            k = op[0]
+            if k == "cos":
+                a = op[2]
+                self.cos.append(self.cos_create(op[1], action=a["action"], queue=a["queue"],
+                                                num_queue=a["num_queue"],
+                                                hash_proto=a["hash_proto"], stats=a["stats"]))
+            elif k == "pmr":
+                self.pmr.append(self.pmr_create(op[1], self.cos[op[2]], self.cos[op[3]], op[4]))
+            elif k == "pmr_destroy":
+                self.L.odp_cls_pmr_destroy(self.pmr[op[1]])
+            elif k == "cos_destroy":
+                self.L.odp_cos_destroy(self.cos[op[1]])
+            elif k == "default":
+                self.L.odp_pktio_default_cos_set(self.pktio, 0 if op[1] is None else self.cos[op[1]])
+            elif k == "error":
+                self.L.odp_pktio_error_cos_set(self.pktio, 0 if op[1] is None else self.cos[op[1]])
+            else:
+                raise ValueError(op)
+        return self.cos, self.pmr
+
+    def compile(self) -> bytes:
+        n = self.L.odp_amd_cls_compile(self.pktio, None, 0)
+        buf = C.create_string_buffer(n)
+        assert self.L.odp_amd_cls_compile(self.pktio, buf, n) == n
+        return buf.raw
+
+    # -- data path -------------------------------------------------------
+    def classify_device(self, d_buf, d_off, d_len, n, d_out, stream=0):
+        """Batch classify on device pointers (ints).  Returns the C status."""
+        return self.L.odp_amd_cls_classify(self.pktio, d_buf, d_off, d_len, n, d_out, stream)
+
+    def classify(self, batch, device="cuda:0"):
+        """Convenience: upload a pktgen.Batch, classify, return a numpy
+        structured array of result records (RESULT_DTYPE)."""
+        import torch
+        dev = torch.device(device)
+        t_buf = torch.from_numpy(np.ascontiguousarray(batch.buf)).to(dev)
+        t_off = torch.from_numpy(batch.off.astype(np.int32, copy=False).view(np.int32)).to(dev)
+        t_len = torch.from_numpy(batch.len.astype(np.int16, copy=False).view(np.int16)).to(dev)
+        t_out = torch.empty((max(1, batch.n), 4), dtype=torch.int32, device=dev)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        rc = self.classify_device(t_buf.data_ptr(), t_off.data_ptr(), t_len.data_ptr(), batch.n,
+                                  t_out.data_ptr(), stream)
+        if rc != 0:
+            raise RuntimeError(f"odp_amd_cls_classify: {rc} "
+                               f"({self.L.mi_cls_strerror(rc).decode()})")
+        torch.cuda.synchronize(dev)
+        out = t_out.cpu().numpy().view(np.uint8).reshape(-1)[: 16 * batch.n]
+        return out.view(R.RESULT_DTYPE).copy()
+
+    def cos_stats_packets(self, cos_handle):
+        s = CosStats()
+        assert self.L.odp_cls_cos_stats(cos_handle, C.byref(s)) == 0
+        return s.packets

@@ -1,0 +1,334 @@
+"""Packet zoo and rule zoo for parity tests.
+
+Frames cover every parser branch of platform/linux-generic/odp_parse.c and
+the bit-exactness quirks listed in SURVEY.md Appendix A; rule programs cover
+every supported PMR term (odp_classification.c:931-1357), chains, marks,
+drop / error CoS, hash queues, deletes and CoS re-creation.
+"""
+import json
+import os
+import struct
+
+import numpy as np
+
+from odp_amd import pktgen as pg
+from odp_amd import rules as R
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def golden_frames():
+    with open(os.path.join(GOLDEN, "parse_frames.json")) as f:
+        d = json.load(f)
+    out = [(k, bytes.fromhex(v["frame"])) for k, v in sorted(d["frames"].items())]
+    out += [(k, bytes.fromhex(v["frame"])) for k, v in sorted(d["other_frames"].items())]
+    return out
+
+
+def udp64_frames():
+    with open(os.path.join(GOLDEN, "udp64.json")) as f:
+        d = json.load(f)
+    return [bytes.fromhex(h) for h in d["frames"]]
+
+
+def quirk_frames():
+    F = []
+    E = pg.eth()
+    # Appendix A 6: tot_len == 20 (< IHL*4 + UDP) still parses UDP
+    F.append(("tot_len_20_udp", pg.pad_to(E + pg.ipv4(tot_len=20) + pg.udp(1234, 2048), 60)))
+    # A 7: non-first fragment; payload bytes 2-3 = 0x0800 (UDP_DPORT 2048 quirk)
+    F.append(("nonfirst_frag_udp", pg.pad_to(
+        E + pg.ipv4(frag=10, payload_len=26) + struct.pack("!HH", 7, 0x0800) + bytes(22), 60)))
+    F.append(("first_frag_mf_udp", pg.udp4_frame(frag=0x2000)))
+    F.append(("frag_tcp_nonfirst", pg.pad_to(E + pg.ipv4(proto=6, frag=0x2005, payload_len=26) +
+                                             bytes(26), 60)))
+    # A 15: single 0x88A8 tag, ETHTYPE_X reads bytes 20-21
+    F.append(("qinq_one_tag", pg.udp4_frame(tags=(0x0123,), tpids=[pg.ETH_QINQ], size=64)))
+    F.append(("qinq_two_tags", pg.udp4_frame(tags=(0x0123, 0x0456), size=68)))
+    F.append(("vlan_pcp5_vid77", pg.udp4_frame(tags=((5 << 13) | 77,), size=64)))
+    F.append(("vlan_in_vlan", pg.udp4_frame(tags=(0x111, 0x222), tpids=[pg.ETH_VLAN, pg.ETH_VLAN],
+                                            size=68)))
+    # A 16: CUSTOM_FRAME gate len > off+sz
+    base = pg.udp4_frame(size=60)
+    F.append(("len60", base))
+    F.append(("len61", base + b"\xaa"))
+    F.append(("len62", base + b"\xaa\xbb"))
+    # A 9: IPv6 + HBH(8) + UDP, payload_len 16 -> ip_err; 64 -> ok
+    hbh = pg.ipv6_ext(pg.IPPROTO_UDP, 0)
+    F.append(("ipv6_hbh_plen16", pg.pad_to(pg.eth(ethtype=pg.ETH_IPV6) +
+                                           pg.ipv6(next_hdr=0, payload_len=16) + hbh +
+                                           pg.udp(5, 6, 8), 120)))
+    F.append(("ipv6_hbh_plen64", pg.pad_to(pg.eth(ethtype=pg.ETH_IPV6) +
+                                           pg.ipv6(next_hdr=0, payload_len=64) + hbh +
+                                           pg.udp(5, 6, 56), 120)))
+    # IPv6 chain HBH -> RH -> RH -> UDP, chain pushing L4 past the 128-B window
+    ch = pg.ipv6_ext(43, 0) + pg.ipv6_ext(43, 4) + pg.ipv6_ext(43, 6, b"\x01\x02") + \
+        pg.ipv6_ext(pg.IPPROTO_UDP, 0)
+    F.append(("ipv6_long_chain", pg.pad_to(pg.eth(ethtype=pg.ETH_IPV6) +
+                                           pg.ipv6(next_hdr=0, payload_len=len(ch) + 40) + ch +
+                                           pg.udp(1111, 2222, 40) + bytes(32), 260)))
+    F.append(("ipv6_frag_direct", pg.pad_to(pg.eth(ethtype=pg.ETH_IPV6) +
+                                            pg.ipv6(next_hdr=44, payload_len=16) + bytes(16), 80)))
+    F.append(("ipv6_hbh_frag", pg.pad_to(pg.eth(ethtype=pg.ETH_IPV6) +
+                                         pg.ipv6(next_hdr=0, payload_len=32) +
+                                         pg.ipv6_ext(44, 0) + bytes(24), 100)))
+    F.append(("ipv6_nonext", pg.pad_to(pg.eth(ethtype=pg.ETH_IPV6) +
+                                       pg.ipv6(next_hdr=59, payload_len=8) + bytes(8), 70)))
+    F.append(("ipv6_bad_ver", pg.pad_to(pg.eth(ethtype=pg.ETH_IPV6) +
+                                        pg.ipv6(ver=4, payload_len=8) + bytes(8), 70)))
+    F.append(("ipv6_plen_too_big", pg.pad_to(pg.eth(ethtype=pg.ETH_IPV6) +
+                                             pg.ipv6(payload_len=400) + bytes(8), 70)))
+    F.append(("ipv6_tc_dscp", pg.udp6_frame(tc=0xb8)))
+    F.append(("ipv6_mcast", pg.udp6_frame(dst="ff02::1")))
+    F.append(("ipv6_sctp", pg.pad_to(pg.eth(ethtype=pg.ETH_IPV6) +
+                                     pg.ipv6(next_hdr=132, payload_len=16) + pg.sctp() + bytes(4), 80)))
+    F.append(("ipv6_tcp_dport", pg.pad_to(pg.eth(ethtype=pg.ETH_IPV6) +
+                                          pg.ipv6(next_hdr=6, payload_len=20) + pg.tcp(5000, 80), 80)))
+    # A 10: truncated UDP (tot_len 26, 40 B frame) -> parse -1; tot_len too big -> ip_err
+    F.append(("udp_truncated", (E + pg.ipv4(tot_len=26) + bytes(6))[:40]))
+    F.append(("ip_totlen_too_big", pg.pad_to(E + pg.ipv4(tot_len=200) + pg.udp(), 60)))
+    F.append(("ip_bad_version", pg.pad_to(E + pg.ipv4(ver=5, payload_len=8) + pg.udp(), 60)))
+    F.append(("ip_ihl4", pg.pad_to(E + pg.ipv4(ihl=4, payload_len=8) + pg.udp(), 60)))
+    F.append(("ip_opts_ihl15", pg.pad_to(E + pg.ipv4(options=bytes([1]) * 40, payload_len=8) +
+                                         pg.udp(3, 4), 90)))
+    F.append(("ip_opts_ihl15_tcp", pg.pad_to(E + pg.ipv4(proto=6, options=bytes([1]) * 40,
+                                                         payload_len=20) + pg.tcp(3, 4), 110)))
+    F.append(("tcp_truncated", (E + pg.ipv4(proto=6, payload_len=20) + pg.tcp())[:50]))
+    F.append(("tcp_hl4", pg.pad_to(E + pg.ipv4(proto=6, payload_len=20) + pg.tcp(hl=4) +
+                                   bytes(4), 60)))
+    F.append(("udp_len7", pg.pad_to(E + pg.ipv4(payload_len=8) + pg.udp(length=7), 60)))
+    F.append(("sctp_ok", pg.pad_to(E + pg.ipv4(proto=132, payload_len=12) + pg.sctp(), 60)))
+    F.append(("sctp_truncated", (E + pg.ipv4(proto=132, payload_len=12) + pg.sctp())[:44]))
+    F.append(("natt_marker", pg.pad_to(E + pg.ipv4(payload_len=16) +
+                                       pg.udp(4500, 4500, 16, b"\x00\x00\x12\x34" + bytes(4)), 60)))
+    F.append(("natt_zero_marker", pg.pad_to(E + pg.ipv4(payload_len=16) +
+                                            pg.udp(4500, 4500, 16, bytes(8)), 60)))
+    F.append(("ah4", pg.pad_to(E + pg.ipv4(proto=51, payload_len=24) + pg.ah(0x11223344), 80)))
+    F.append(("esp4", pg.pad_to(E + pg.ipv4(proto=50, payload_len=8) + pg.esp(0x55667788), 60)))
+    F.append(("ah6", pg.pad_to(pg.eth(ethtype=pg.ETH_IPV6) + pg.ipv6(next_hdr=51, payload_len=24) +
+                               pg.ah(0x0a0b0c0d), 100)))
+    F.append(("esp6", pg.pad_to(pg.eth(ethtype=pg.ETH_IPV6) + pg.ipv6(next_hdr=50, payload_len=8) +
+                                pg.esp(0x01020304), 80)))
+    F.append(("ipip", pg.pad_to(E + pg.ipv4(proto=4, payload_len=20) + pg.ipv4(), 60)))
+    F.append(("icmp4", pg.pad_to(E + pg.ipv4(proto=1, payload_len=8) + pg.icmp(), 60)))
+    F.append(("igmp", pg.pad_to(E + pg.ipv4(proto=2, payload_len=8) + bytes(8), 60)))
+    F.append(("ip_bcast", pg.udp4_frame(dst="255.255.255.255")))
+    F.append(("ip_mcast", pg.udp4_frame(dst="239.1.2.3")))
+    F.append(("eth_bcast", pg.udp4_frame(dmac=b"\xff" * 6)))
+    F.append(("eth_mcast", pg.udp4_frame(dmac=b"\x01\x00\x5e\x00\x00\x01")))
+    F.append(("dscp46", pg.udp4_frame(tos=46 << 2)))
+    F.append(("arp", pg.pad_to(pg.eth(ethtype=pg.ETH_ARP) + bytes(28), 60)))
+    F.append(("unknown_ethtype", pg.pad_to(pg.eth(ethtype=0x88B5) + bytes(40), 60)))
+    # SNAP: length field 0x30 (ok), 0x0500 > remaining (snap_len_err)
+    F.append(("snap_ok", pg.pad_to(pg.eth(ethtype=0x30) + b"\xaa\xaa\x03\x00\x00\x00\x08\x00" +
+                                   pg.ipv4(payload_len=8) + pg.udp(), 64)))
+    F.append(("snap_len_err", pg.pad_to(pg.eth(ethtype=0x0500) + bytes(40), 60)))
+    F.append(("snap_vlan", pg.pad_to(pg.eth(ethtype=0x30) + b"\xaa\xaa\x03\x00\x00\x00\x81\x00" +
+                                     b"\x00\x05\x08\x00" + pg.ipv4(payload_len=8) + pg.udp(), 72)))
+    # jumbo
+    F.append(("jumbo_udp", pg.udp4_frame(size=1600)))
+    F.append(("jumbo_9000", pg.udp4_frame(size=9000)))
+    # short frames: every length 0..24 of a tagged IPv4/UDP frame
+    full = pg.udp4_frame(tags=(0x0ABC,), size=64)
+    for n in (0, 1, 5, 6, 11, 12, 13, 14, 15, 17, 18, 19, 20, 21, 22, 24, 30, 37, 38, 41, 45):
+        F.append((f"short_{n}", full[:n]))
+    # custom-offset windows beyond 128 B (global-memory path)
+    big = bytearray(pg.udp4_frame(size=300))
+    for i in range(100, 300):
+        big[i] = i & 0xFF
+    F.append(("big300_pattern", bytes(big)))
+    # TCP / UDP port variety
+    for sp, dp in ((1024, 2048), (80, 8080), (4000, 4001), (3000, 3001), (65535, 0)):
+        F.append((f"udp_{sp}_{dp}", pg.udp4_frame(sport=sp, dport=dp)))
+        F.append((f"tcp_{sp}_{dp}", pg.tcp4_frame(sport=sp, dport=dp)))
+    for s in ("10.0.0.1", "10.0.0.5", "10.0.0.6", "10.0.0.7", "10.10.10.1", "192.168.1.7"):
+        F.append((f"sip_{s}", pg.udp4_frame(src=s, dst="10.0.0.100")))
+    return F
+
+
+def all_frames():
+    F = golden_frames() + [("udp64_%d" % i, f) for i, f in enumerate(udp64_frames()[:2])]
+    return F + quirk_frames()
+
+
+def zoo_batch(frames=None):
+    frames = frames or all_frames()
+    return pg.batch_from_frames([f for _, f in frames]), [n for n, _ in frames]
+
+
+# ----------------------------------------------------------- rule programs
+def term_examples():
+    """One (name, term tuple) per supported term, with values taken from zoo
+    frames so that each matches something."""
+    T = []
+    T.append(("len60", R.t_len(60)))
+    T.append(("len_mask", R.t_len(0x0100, 0xFF00)))        # odp_classification_test_pmr.c:980-1011
+    T.append(("eth0_ipv6", R.t_be16(R.PMR_ETHTYPE_0, pg.ETH_IPV6)))
+    T.append(("ethx_ipv4", R.t_be16(R.PMR_ETHTYPE_X, pg.ETH_IPV4)))
+    T.append(("ethx_4500", R.t_be16(R.PMR_ETHTYPE_X, 0x4500)))  # qinq one-tag quirk
+    T.append(("vid0_77", R.t_be16(R.PMR_VLAN_ID_0, 77)))
+    T.append(("vid0_0123", R.t_be16(R.PMR_VLAN_ID_0, 0x123)))
+    T.append(("vidx_0456", R.t_be16(R.PMR_VLAN_ID_X, 0x456)))
+    T.append(("vidx_0123", R.t_be16(R.PMR_VLAN_ID_X, 0x123)))
+    T.append(("vidx_0x0800mask", R.t_be16(R.PMR_VLAN_ID_X, 0x0800, 0x0F00)))
+    T.append(("pcp5", R.t_u8(R.PMR_VLAN_PCP_0, 5)))
+    T.append(("dmac_bcast", (R.PMR_DMAC, b"\xff" * 6, b"\xff" * 6, 0)))
+    T.append(("dmac_mcast_bit", (R.PMR_DMAC, b"\x01" + bytes(5), b"\x01" + bytes(5), 0)))
+    T.append(("proto_tcp", R.t_u8(R.PMR_IPPROTO, 6)))
+    T.append(("proto_udp", R.t_u8(R.PMR_IPPROTO, 17)))
+    T.append(("proto_hbh_v6", R.t_u8(R.PMR_IPPROTO, 0)))   # IPv6 fixed next_hdr quirk
+    T.append(("dscp46", R.t_u8(R.PMR_IP_DSCP, 46)))
+    T.append(("dscp_v6", R.t_u8(R.PMR_IP_DSCP, 0xb8 >> 2)))
+    T.append(("udp_dport2048", R.t_be16(R.PMR_UDP_DPORT, 2048)))
+    T.append(("udp_dport4001", R.t_be16(R.PMR_UDP_DPORT, 4001)))
+    T.append(("udp_sport_1024", R.t_be16(R.PMR_UDP_SPORT, 1024)))
+    T.append(("tcp_dport80", R.t_be16(R.PMR_TCP_DPORT, 80)))
+    T.append(("tcp_dport4001", R.t_be16(R.PMR_TCP_DPORT, 4001)))
+    T.append(("tcp_sport5000", R.t_be16(R.PMR_TCP_SPORT, 5000)))
+    T.append(("tcp_sport_mask", R.t_be16(R.PMR_TCP_SPORT, 0x0400, 0xFF00)))
+    T.append(("sip_10_0_0_5", R.t_ip4(R.PMR_SIP_ADDR, "10.0.0.5", 32)))
+    T.append(("sip_10_8", R.t_ip4(R.PMR_SIP_ADDR, "10.0.0.0", 8)))
+    T.append(("dip_bcast", R.t_ip4(R.PMR_DIP_ADDR, "255.255.255.255", 32)))
+    T.append(("dip_10_0_0_100", R.t_ip4(R.PMR_DIP_ADDR, "10.0.0.100", 32)))
+    T.append(("sip6_db8", R.t_ip6(R.PMR_SIP6_ADDR, "2001:db8::", 32)))
+    T.append(("dip6_2", R.t_ip6(R.PMR_DIP6_ADDR, "2001:db8::2", 128)))
+    T.append(("dip6_ff02", R.t_ip6(R.PMR_DIP6_ADDR, "ff02::", 16)))
+    T.append(("spi_ah4", (R.PMR_IPSEC_SPI, struct.pack("!I", 0x11223344), b"\xff" * 4, 0)))
+    T.append(("spi_esp6", (R.PMR_IPSEC_SPI, struct.pack("!I", 0x01020304), b"\xff" * 4, 0)))
+    T.append(("ld_vni", (R.PMR_LD_VNI, bytes(4), bytes(4), 0)))   # never matches
+    T.append(("custom_58_2", R.t_custom(R.PMR_CUSTOM_FRAME, 58, b"\xaa\xbb", b"\xff\xff")))
+    T.append(("custom_58_1", R.t_custom(R.PMR_CUSTOM_FRAME, 58, b"\x00", b"\x00")))
+    T.append(("custom_frame_ip", R.t_custom(R.PMR_CUSTOM_FRAME, 26, pg.ip4("10.0.0.5"),
+                                            b"\xff\xff\xff\xff")))
+    T.append(("custom_frame_far", R.t_custom(R.PMR_CUSTOM_FRAME, 200, bytes(range(200, 216)),
+                                             b"\xff" * 16)))
+    T.append(("custom_frame_far7", R.t_custom(R.PMR_CUSTOM_FRAME, 253, bytes(range(253, 256)) +
+                                              bytes(range(0, 4)), b"\xff" * 7)))
+    T.append(("custom_l3_sip", R.t_custom(R.PMR_CUSTOM_L3, 12, pg.ip4("10.0.0.6"),
+                                          b"\xff\xff\xff\xff")))
+    T.append(("custom_l3_zero", R.t_custom(R.PMR_CUSTOM_L3, 0, b"", b"")))
+    T.append(("custom_l3_far", R.t_custom(R.PMR_CUSTOM_L3, 150, bytes([164, 165, 166]), b"\xff\xfe\xff")))
+    return T
+
+
+def prog_single(term, extra_terms=(), mark=0):
+    """default CoS + one PMR -> 'hit' CoS (test_pmr pattern,
+    odp_classification_test_pmr.c:678-719)."""
+    return [R.cos("default", queue=11), R.cos("hit", queue=22), ("default", 0),
+            ("pmr", [term, *extra_terms], 0, 1, mark)]
+
+
+def prog_everything():
+    """All terms flat on the default CoS, plus chain / mark / drop / error /
+    hash-queue CoS."""
+    p = [R.cos("default", queue=1), R.cos("err", queue=2), R.cos("drop", action=1),
+         R.cos("hashq4", num_queue=4, hash_proto=R.HP_IPV4_UDP | R.HP_IPV6_UDP),
+         R.cos("hashq_all", num_queue=7, hash_proto=R.HP_IPV4 | R.HP_IPV6 | R.HP_IPV4_TCP |
+               R.HP_IPV6_TCP | R.HP_IPV4_UDP | R.HP_IPV6_UDP)]
+    ex = term_examples()
+    base = len(p)
+    for i, (name, _) in enumerate(ex):
+        p.append(R.cos(name, queue=100 + i, stats=i % 2))
+    p.append(("default", 0))
+    p.append(("error", 1))
+    p.append(("pmr", [R.t_be16(R.PMR_UDP_DPORT, 4001)], 0, 2, 0))       # drop (CLS_DROP_PORT)
+    p.append(("pmr", [R.t_ip4(R.PMR_SIP_ADDR, "10.0.0.7", 32)], 0, 3, 7))
+    p.append(("pmr", [R.t_be16(R.PMR_TCP_DPORT, 8080)], 0, 4, 0))
+    for i, (name, t) in enumerate(ex):
+        p.append(("pmr", [t], 0, base + i, (i * 37) & 0xFFFF))
+    # chain: sip 10/8 CoS -> dport CoS (configure_cls_pmr_chain, tests.c:320-458)
+    ci = [n for n, _ in ex].index("sip_10_8")
+    p.append(("pmr", [R.t_be16(R.PMR_UDP_DPORT, 3001)], base + ci, 3, 0))
+    p.append(("pmr", [R.t_be16(R.PMR_UDP_SPORT, 1024), R.t_u8(R.PMR_IPPROTO, 17)], base + ci,
+              base, 0x1234))
+    return p
+
+
+def prog_deletes():
+    """Swap-on-delete order, CoS destroy (skipped link), CoS re-create."""
+    p = [R.cos("default", queue=1)]
+    for i in range(6):
+        p.append(R.cos(f"c{i}", queue=10 + i))
+    p.append(("default", 0))
+    terms = [R.t_ip4(R.PMR_SIP_ADDR, "10.0.0.0", 8), R.t_be16(R.PMR_UDP_DPORT, 2048),
+             R.t_u8(R.PMR_IPPROTO, 17), R.t_be16(R.PMR_UDP_SPORT, 1024),
+             R.t_be16(R.PMR_ETHTYPE_0, pg.ETH_IPV4), R.t_len(60)]
+    for i, t in enumerate(terms):
+        p.append(("pmr", [t], 0, 1 + i, i))
+    p.append(("pmr_destroy", 0))       # last (len60 -> c5) moves into slot 0
+    p.append(("cos_destroy", 5))       # c4 (ethtype) link becomes invalid -> skipped
+    p.append(("pmr_destroy", 2))
+    p.append(R.cos("new", queue=99))   # takes the lowest free slot (c4's)
+    p.append(("pmr", [R.t_be16(R.PMR_UDP_DPORT, 4000)], 0, 7, 42))
+    return p
+
+
+def prog_loop():
+    """CoS cycle A -> B -> A (the reference never returns; both sides here
+    report OUT_LOOP after max_hops)."""
+    return [R.cos("default", queue=1), R.cos("A", queue=2), R.cos("B", queue=3), ("default", 0),
+            ("pmr", [R.t_u8(R.PMR_IPPROTO, 17)], 0, 1, 0),
+            ("pmr", [R.t_u8(R.PMR_IPPROTO, 17)], 1, 2, 5),
+            ("pmr", [R.t_u8(R.PMR_IPPROTO, 17)], 2, 1, 6),
+            ("pmr", [R.t_u8(R.PMR_IPPROTO, 6)], 0, 0, 9)]   # TCP: back to default (default cycle)
+
+
+def prog_no_default():
+    return [R.cos("a", queue=1), R.cos("err", action=1), ("error", 1)]
+
+
+def random_program(rng, frames, n_cos=12, n_rules=60, with_deletes=True):
+    """Random CoS graph with random terms whose values come from zoo frames
+    (so that they match), random masks, random marks."""
+    ex = [t for _, t in term_examples()]
+    p = [R.cos("default", queue=1)]
+    for i in range(1, n_cos):
+        r = rng.random()
+        if r < 0.1:
+            p.append(R.cos(f"d{i}", action=1))
+        elif r < 0.25:
+            p.append(R.cos(f"h{i}", num_queue=int(rng.integers(2, 33)),
+                           hash_proto=int(rng.integers(1, 64)), stats=int(rng.integers(0, 2))))
+        else:
+            p.append(R.cos(f"c{i}", queue=100 + i, stats=int(rng.integers(0, 2))))
+    p.append(("default", 0))
+    if rng.random() < 0.7:
+        p.append(("error", int(rng.integers(0, n_cos))))
+    npmr = 0
+    for _ in range(n_rules):
+        k = int(rng.integers(1, 4))
+        terms = []
+        for _ in range(k):
+            t = ex[int(rng.integers(0, len(ex)))]
+            term, val, mask, off = t
+            if rng.random() < 0.3 and len(val):
+                mask = bytes(int(b) & int(rng.integers(0, 256)) for b in mask)
+            terms.append((term, val, mask, off))
+        # mostly a DAG (src < dst) so descents terminate
+        src = int(rng.integers(0, n_cos - 1))
+        dst = int(rng.integers(src + 1, n_cos))
+        p.append(("pmr", terms, src, dst, int(rng.integers(0, 65536)) if rng.random() < 0.5 else 0))
+        npmr += 1
+    if with_deletes:
+        for _ in range(int(rng.integers(0, 6))):
+            p.append(("pmr_destroy", int(rng.integers(0, npmr))))
+        if rng.random() < 0.3:
+            p.append(("cos_destroy", int(rng.integers(1, n_cos))))
+    return p
+
+
+def mutate_frames(rng, frames, n):
+    """Random header-byte mutations of zoo frames (fuzz)."""
+    out = []
+    for i in range(n):
+        f = bytearray(frames[int(rng.integers(0, len(frames)))])
+        if len(f) == 0:
+            out.append(bytes(f))
+            continue
+        for _ in range(int(rng.integers(1, 4))):
+            j = int(rng.integers(0, min(len(f), 80)))
+            f[j] = int(rng.integers(0, 256))
+        if rng.random() < 0.2:
+            f = f[: int(rng.integers(0, len(f) + 1))]
+        out.append(bytes(f))
+    return out
