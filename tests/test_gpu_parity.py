@@ -9,6 +9,7 @@ import pytest
 
 from odp_amd import pktgen as pg
 from odp_amd import rules as R
+from tests import refcases as RC
 from tests import zoo
 from tests.helpers import assert_same, gpu_run, oracle_run, summary
 
@@ -183,3 +184,23 @@ def test_config3_full_size_properties(built, gpu):
     assert np.all(got["l3_offset"] == 14) and np.all(got["l4_offset"] == 34)
     # determinism: a second run is identical
     assert np.array_equal(got, gpu_run(prog, b))
+
+
+@pytest.mark.parametrize("case", RC.term_cases() + RC.chain_cases(), ids=lambda c: c[0])
+def test_reference_known_answers_gpu(built, gpu, case):
+    """The reference validation suite's MATCH / NO_MATCH expectations on the
+    HIP path (odp_classification_test_pmr.c, odp_classification_tests.c)."""
+    name, prog, pkts = case
+    b = pg.batch_from_frames([f for f, _ in pkts])
+    got = both(prog, b, what=name)
+    assert list(got["cos"]) == [e for _, e in pkts]
+
+
+def test_parser_frames_gpu(built, gpu):
+    """Parser frames of test/common/test_packet_*.h: every flag word, error
+    bit and offset equals the oracle's (which test_oracle_golden pins to
+    packet.c's assertions)."""
+    frames = zoo.golden_frames()
+    b = pg.batch_from_frames([f for _, f in frames])
+    got = both([R.cos("d", queue=1), ("default", 0)], b, what="parser frames")
+    assert np.all(got["outcome"] == R.OUT_ENQ)

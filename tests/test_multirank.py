@@ -1,0 +1,85 @@
+"""World-size-2 rehearsal of the multi-GPU path on CPU (gloo): each rank
+classifies its own contiguous shard (here with the CPU oracle standing in for
+the per-GPU kernel, which needs a device), results gathered in rank order
+must equal the single-process run, and the bench's max-over-ranks timing
+reduction is exercised with the same collective calls the GPU run makes."""
+import os
+import socket
+
+import numpy as np
+import torch.multiprocessing as mp
+
+from odp_amd import rules as R
+from odp_amd.shard import shard_bounds
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, cfg, n, q):
+    import torch
+    import torch.distributed as dist
+    from tests.helpers import oracle_run
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    batch, prog = R.CONFIGS[cfg](n)
+    b, e = shard_bounds(batch.len, world)[rank]
+    res, _ = oracle_run(prog, batch.slice(b, e))
+    rec = torch.from_numpy(res.view(np.uint8).copy())
+    sizes = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(sizes, torch.tensor([rec.numel()]))
+    mx = int(max(s.item() for s in sizes))
+    pad = torch.zeros(mx, dtype=torch.uint8)
+    pad[: rec.numel()] = rec
+    bufs = [torch.zeros(mx, dtype=torch.uint8) for _ in range(world)]
+    dist.all_gather(bufs, pad)
+    t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)          # bench.py's timing reduction
+    dist.barrier()
+    if rank == 0:
+        out = np.concatenate([bufs[r][: int(sizes[r].item())].numpy() for r in range(world)])
+        q.put((out.view(R.RESULT_DTYPE), t.item()))
+    dist.destroy_process_group()
+
+
+def _run(cfg, n, world=2):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, cfg, n, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got, tmax = q.get(timeout=300)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return got, tmax
+
+
+def test_shard_bounds_balanced():
+    lens = np.array([60] * 700 + [1514] * 100 + [566] * 200)
+    rng = np.random.default_rng(0)
+    rng.shuffle(lens)
+    for world in (1, 2, 3, 8):
+        b = shard_bounds(lens, world)
+        assert b[0][0] == 0 and b[-1][1] == len(lens)
+        assert all(b[i][1] == b[i + 1][0] for i in range(world - 1))
+        w = np.minimum(lens, 128) + 22
+        parts = [w[s:e].sum() for s, e in b]
+        assert max(parts) - min(parts) <= 2 * 150   # each cut is within one packet
+
+
+def test_two_rank_shards_equal_single(built):
+    from tests.helpers import oracle_run
+    for cfg, n in ((3, 3000), (4, 2000)):
+        got, tmax = _run(cfg, n)
+        batch, prog = R.CONFIGS[cfg](n)
+        exp, _ = oracle_run(prog, batch)
+        assert np.array_equal(got, exp)
+        assert tmax == 2.0
