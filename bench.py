@@ -61,6 +61,11 @@ def make_workload(cfg, n, rank):
         return R.config1(n)
     if cfg == 33:   # 64 B packets, 256 L3+L4 rules (north-star target case)
         return R.config3(n, size=60, rank=rank)
+    if cfg == 20:   # config 2 traffic, default CoS only (parse + stage floor)
+        b, p = R.config2(n, rank=rank)
+        return b, [op for op in p if op[0] != "pmr"]
+    if cfg == 34:   # config 3 IMIX traffic, 64 rules
+        return R.config3(n, num_rules=64, rank=rank)
     raise ValueError(cfg)
 
 

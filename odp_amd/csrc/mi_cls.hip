@@ -32,6 +32,10 @@
 
 #include "mi_cls.h"
 
+#include <array>
+#include <map>
+#include <vector>
+
 #define WAVE 64
 #define WAVES_PER_BLOCK 4
 #define BLOCK (WAVE * WAVES_PER_BLOCK)
@@ -427,71 +431,63 @@ __device__ uint32_t rss_hash(const Pkt &k, const Parsed &p, uint32_t hp)
 	return h;
 }
 
-// ----------------------------------------------------------- term verifier
+// ------------------------------------------------------ device rule program
+// mi_cls_rules_load() assembles the mi_cls.h table into this private,
+// read-only encoding, read by the kernel through the constant address space
+// (scalar loads: every lane of a wave tests the same rule):
+//
+//   words [0, 16)          header  (DH_* below)
+//   words [cos_off, ...)   8 words per CoS slot: rule record index, #rules,
+//                          meta = action | num_queue<<8 | hash_proto<<16 | index<<24,
+//                          valid, bit-vector block offset (0 = linear scan)
+//   words [prog_off, ...)  16-word rule records, CoS rules contiguous in scan order:
+//        w0  = inline terms | ext terms<<4 | mark<<16
+//        w1  = dst CoS | ext word offset<<8
+//        w2.. terms: op word (kind | size<<8 | nw<<16), [offset word for custom
+//             kinds], then nw (mask, value) word pairs; terms that do not fit
+//             the 14 inline words continue at the ext offset.
+typedef const __attribute__((address_space(4))) uint32_t *cword_t;
+
+enum { DH_MAGIC = 0, DH_NCOS, DH_DEFAULT, DH_ERROR, DH_DEFAULT_VALID, DH_USED, DH_MAX_HOPS,
+       DH_COS_OFF, DH_PROG_OFF, DH_TOTAL, DH_WORDS = 16 };
+#define DEV_MAGIC 0x32564544u   // "DEV2"
+#define REC_WORDS 16u
+#define COS_WORDS 8u
+#define BV_MAX_CLS 8u
+#define BV_CLS_WORDS 16u
+#define BV_EMPTY 0xFFFFFFFFu
+
+// Bit-vector (BV) block of a CoS, used when its rules fall into at most
+// BV_MAX_CLS key classes.  A key class is one (term kind, mask[, offset,
+// size]) combination; for every class the block holds a hash table
+// key -> bitmap row over the CoS's rules (bit r = rule r's terms of that
+// class all equal the key, or rule r has no term of that class), row 0 being
+// the "no term of this class" row used when the packet lacks the field.
+// A packet's matching rules are the AND of its rows; the lowest set bit is
+// the first rule in scan order whose every term matches -- exactly the rule
+// match_pmr_cos picks (odp_classification.c:1631-1650).
+//   bv[0] = W (32-bit words per row), bv[1] = #classes, bv[2] = alive row offset
+//   bv[4 + 16 k ...] class k: kind, nkey, 0, offset, size, mask[4],
+//                    table mask, table offset, rows offset
+//   table slot: nkey key words + row index (BV_EMPTY = free slot)
+
 __device__ __forceinline__ bool eq1(uint32_t x, uint32_t m, uint32_t v)
 {
 	return (x & m) == v;
 }
 
-// verify one compiled term (all wave-uniform inputs in SGPRs except the
-// packet fields); the kind switch is a scalar branch.
-__device__ __forceinline__ bool term_ok(const mi_term_t *__restrict__ t, const Pkt &k,
-					const Parsed &p, const Fields &x)
+// verify_pmr_<term> for one term whose words start at prog[q] (uniform);
+// returns the lane's verdict and advances q past the term.
+__device__ __forceinline__ bool term_ok(cword_t prog, uint32_t &q, const Pkt &k, const Parsed &p,
+					const Fields &x)
 {
-	const uint32_t kind = __builtin_amdgcn_readfirstlane(t->kind);
-	const uint32_t m0 = __builtin_amdgcn_readfirstlane(t->mask[0]);
-	const uint32_t v0 = __builtin_amdgcn_readfirstlane(t->value[0]);
+	const uint32_t op = prog[q];
+	const uint32_t kind = op & 0xffu;
 	const uint32_t g = x.gates;
-	switch (kind) {
-	case MI_K_LEN:
-		return eq1(k.len, m0, v0);
-	case MI_K_ETH0:
-		return (g & G_ETH) && eq1(x.eth0, m0, v0);
-	case MI_K_ETHX:
-		return (g & G_VLANX) && eq1(x.ethx, m0, v0);
-	case MI_K_VID0:
-		return (g & G_VLAN0) && eq1(x.vid0, m0, v0);
-	case MI_K_VIDX:
-		return (g & G_VLANX) && eq1(x.vidx, m0, v0);
-	case MI_K_PCP0:
-		return (g & G_VLAN0) && eq1(x.pcp0, m0, v0);
-	case MI_K_DMAC: {
-		const uint32_t m1 = __builtin_amdgcn_readfirstlane(t->mask[1]);
-		const uint32_t v1 = __builtin_amdgcn_readfirstlane(t->value[1]);
-		return (g & G_ETH) && eq1(x.dmac0, m0, v0) && eq1(x.dmac1, m1, v1);
-	}
-	case MI_K_PROTO:
-		return (g & (G_V4 | G_V6)) && eq1(x.proto, m0, v0);
-	case MI_K_DSCP:
-		return (g & (G_V4 | G_V6)) && eq1(x.dscp, m0, v0);
-	case MI_K_UDP_DPORT:
-	case MI_K_UDP_SPORT:
-		return (g & G_UDP) && eq1(x.ports, m0, v0);
-	case MI_K_TCP_DPORT:
-	case MI_K_TCP_SPORT:
-		return (g & G_TCP) && eq1(x.ports, m0, v0);
-	case MI_K_SIP:
-		return (g & G_V4) && eq1(x.sip, m0, v0);
-	case MI_K_DIP:
-		return (g & G_V4) && eq1(x.dip, m0, v0);
-	case MI_K_SIP6:
-	case MI_K_DIP6: {
-		const uint32_t *a = (kind == MI_K_SIP6) ? x.s6 : x.d6;
-		bool ok = (g & G_V6) && eq1(a[0], m0, v0);
-#pragma unroll
-		for (int i = 1; i < 4; ++i) {
-			const uint32_t mi = __builtin_amdgcn_readfirstlane(t->mask[i]);
-			const uint32_t vi = __builtin_amdgcn_readfirstlane(t->value[i]);
-			ok = ok && eq1(a[i], mi, vi);
-		}
-		return ok;
-	}
-	case MI_K_SPI:
-		return (g & G_SPI) && eq1(x.spi, m0, v0);
-	case MI_K_CUSTOM_FRAME:
-	case MI_K_CUSTOM_L3: {
-		const uint32_t toff = __builtin_amdgcn_readfirstlane(t->offset);
-		const uint32_t sz = __builtin_amdgcn_readfirstlane(t->size);
+	if (kind == MI_K_CUSTOM_FRAME || kind == MI_K_CUSTOM_L3) {
+		const uint32_t sz = (op >> 8) & 0xffu;
+		const uint32_t nw = (op >> 16) & 0xffu;
+		const uint32_t toff = prog[q + 1];
 		uint32_t o = toff;
 		bool ok = true;
 		if (kind == MI_K_CUSTOM_L3) {
@@ -501,20 +497,177 @@ __device__ __forceinline__ bool term_ok(const mi_term_t *__restrict__ t, const P
 		// verify_pmr_custom_*: "packet_len <= offset + val_sz" -> no match (u32 math)
 		ok = ok && !(k.len <= o + sz);
 		if (ok) {
-			ok = eq1(r32(k, o), m0, v0);
-#pragma unroll
-			for (int i = 1; i < 4; ++i) {
-				const uint32_t mi = __builtin_amdgcn_readfirstlane(t->mask[i]);
-				const uint32_t vi = __builtin_amdgcn_readfirstlane(t->value[i]);
-				if (sz > 4u * i)
-					ok = ok && eq1(r32(k, o + 4u * i), mi, vi);
+			for (uint32_t i = 0; i < nw; ++i)
+				ok = ok && eq1(r32(k, o + 4u * i), prog[q + 2 + 2 * i], prog[q + 3 + 2 * i]);
+		}
+		q += 2u + 2u * nw;
+		return ok;
+	}
+	const uint32_t m0 = prog[q + 1];
+	const uint32_t v0 = prog[q + 2];
+	bool ok;
+	switch (kind) {
+	case MI_K_LEN:
+		ok = eq1(k.len, m0, v0);
+		break;
+	case MI_K_ETH0:
+		ok = (g & G_ETH) && eq1(x.eth0, m0, v0);
+		break;
+	case MI_K_ETHX:
+		ok = (g & G_VLANX) && eq1(x.ethx, m0, v0);
+		break;
+	case MI_K_VID0:
+		ok = (g & G_VLAN0) && eq1(x.vid0, m0, v0);
+		break;
+	case MI_K_VIDX:
+		ok = (g & G_VLANX) && eq1(x.vidx, m0, v0);
+		break;
+	case MI_K_PCP0:
+		ok = (g & G_VLAN0) && eq1(x.pcp0, m0, v0);
+		break;
+	case MI_K_DMAC:
+		ok = (g & G_ETH) && eq1(x.dmac0, m0, v0) && eq1(x.dmac1, prog[q + 3], prog[q + 4]);
+		q += 2;
+		break;
+	case MI_K_PROTO:
+		ok = (g & (G_V4 | G_V6)) && eq1(x.proto, m0, v0);
+		break;
+	case MI_K_DSCP:
+		ok = (g & (G_V4 | G_V6)) && eq1(x.dscp, m0, v0);
+		break;
+	case MI_K_UDP_DPORT:
+	case MI_K_UDP_SPORT:
+		ok = (g & G_UDP) && eq1(x.ports, m0, v0);
+		break;
+	case MI_K_TCP_DPORT:
+	case MI_K_TCP_SPORT:
+		ok = (g & G_TCP) && eq1(x.ports, m0, v0);
+		break;
+	case MI_K_SIP:
+		ok = (g & G_V4) && eq1(x.sip, m0, v0);
+		break;
+	case MI_K_DIP:
+		ok = (g & G_V4) && eq1(x.dip, m0, v0);
+		break;
+	case MI_K_SIP6:
+	case MI_K_DIP6: {
+		const uint32_t *a = (kind == MI_K_SIP6) ? x.s6 : x.d6;
+		ok = (g & G_V6) && eq1(a[0], m0, v0) && eq1(a[1], prog[q + 3], prog[q + 4]) &&
+		     eq1(a[2], prog[q + 5], prog[q + 6]) && eq1(a[3], prog[q + 7], prog[q + 8]);
+		q += 6;
+		break;
+	}
+	case MI_K_SPI:
+		ok = (g & G_SPI) && eq1(x.spi, m0, v0);
+		break;
+	case MI_K_ALWAYS:
+		ok = true;
+		break;
+	default:   // MI_K_NEVER (LD_VNI)
+		ok = false;
+		break;
+	}
+	q += 3;
+	return ok;
+}
+
+__device__ __forceinline__ uint32_t bv_hash(const uint32_t k[4])
+{
+	uint32_t h = k[0] * 0x9E3779B1u ^ k[1] * 0x85EBCA77u ^ k[2] * 0xC2B2AE3Du ^ k[3] * 0x27D4EB2Fu;
+	h ^= h >> 15;
+	h *= 0x2C1B3C6Du;
+	h ^= h >> 12;
+	return h;
+}
+
+// Key of a packet for one BV class: the masked field the class's terms
+// compare, and whether the packet has that field at all (the term's gate).
+__device__ __forceinline__ bool bv_key(cword_t cr, const Pkt &k, const Parsed &p, const Fields &x,
+				       uint32_t key[4])
+{
+	const uint32_t kind = cr[0];
+	const uint32_t m0 = cr[5], m1 = cr[6], m2 = cr[7], m3 = cr[8];
+	const uint32_t g = x.gates;
+	key[1] = key[2] = key[3] = 0;
+	switch (kind) {
+	case MI_K_LEN:
+		key[0] = k.len & m0;
+		return true;
+	case MI_K_ETH0:
+		key[0] = x.eth0 & m0;
+		return g & G_ETH;
+	case MI_K_ETHX:
+		key[0] = x.ethx & m0;
+		return g & G_VLANX;
+	case MI_K_VID0:
+		key[0] = x.vid0 & m0;
+		return g & G_VLAN0;
+	case MI_K_VIDX:
+		key[0] = x.vidx & m0;
+		return g & G_VLANX;
+	case MI_K_PCP0:
+		key[0] = x.pcp0 & m0;
+		return g & G_VLAN0;
+	case MI_K_DMAC:
+		key[0] = x.dmac0 & m0;
+		key[1] = x.dmac1 & m1;
+		return g & G_ETH;
+	case MI_K_PROTO:
+		key[0] = x.proto & m0;
+		return g & (G_V4 | G_V6);
+	case MI_K_DSCP:
+		key[0] = x.dscp & m0;
+		return g & (G_V4 | G_V6);
+	case MI_K_UDP_DPORT:
+	case MI_K_UDP_SPORT:
+		key[0] = x.ports & m0;
+		return g & G_UDP;
+	case MI_K_TCP_DPORT:
+	case MI_K_TCP_SPORT:
+		key[0] = x.ports & m0;
+		return g & G_TCP;
+	case MI_K_SIP:
+		key[0] = x.sip & m0;
+		return g & G_V4;
+	case MI_K_DIP:
+		key[0] = x.dip & m0;
+		return g & G_V4;
+	case MI_K_SIP6:
+	case MI_K_DIP6: {
+		const uint32_t *a = (kind == MI_K_SIP6) ? x.s6 : x.d6;
+		key[0] = a[0] & m0;
+		key[1] = a[1] & m1;
+		key[2] = a[2] & m2;
+		key[3] = a[3] & m3;
+		return g & G_V6;
+	}
+	case MI_K_SPI:
+		key[0] = x.spi & m0;
+		return g & G_SPI;
+	case MI_K_CUSTOM_FRAME:
+	case MI_K_CUSTOM_L3: {
+		const uint32_t toff = cr[3], sz = cr[4], nk = cr[1];
+		uint32_t o = toff;
+		bool ok = true;
+		if (kind == MI_K_CUSTOM_L3) {
+			ok = (g & G_L3OK) != 0;
+			o = p.l3 + toff;
+		}
+		ok = ok && !(k.len <= o + sz);
+		key[0] = 0;
+		if (ok) {
+			key[0] = r32(k, o) & m0;
+			if (nk > 1)
+				key[1] = r32(k, o + 4) & m1;
+			if (nk > 2) {
+				key[2] = r32(k, o + 8) & m2;
+				key[3] = r32(k, o + 12) & m3;
 			}
 		}
 		return ok;
 	}
-	case MI_K_ALWAYS:
-		return true;
-	default:   // MI_K_NEVER (LD_VNI) and anything unknown
+	default:
+		key[0] = 0;
 		return false;
 	}
 }
@@ -525,15 +678,26 @@ struct KArgs {
 	const uint32_t *off;
 	const uint16_t *len;
 	uint32_t n;
-	const uint8_t *tbl;
+	const uint32_t *dev;         // device rule program (constant address space)
 	mi_cls_result_t *out;
-	unsigned long long *stats;   // num_cos counters, or NULL
+	unsigned long long *stats;   // MAX_STATS_COS counters, or NULL
 	uint32_t stats_mask[8];
 };
 
 __device__ __forceinline__ bool stats_bit(const KArgs &a, uint32_t c)
 {
 	return c < MAX_STATS_COS && ((a.stats_mask[c >> 5] >> (c & 31u)) & 1u);
+}
+
+// Make this wave's LDS writes visible to its own later LDS reads by other
+// lanes: LDS ops of one wave complete in order, so a wave-scope fence (which
+// keeps the compiler from reordering) is all that is needed -- no block
+// barrier, waves run independently.
+__device__ __forceinline__ void wave_lds_sync()
+{
+	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+	__builtin_amdgcn_wave_barrier();
+	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 __global__ __launch_bounds__(BLOCK) void mi_cls_kernel(KArgs a)
@@ -545,72 +709,76 @@ __global__ __launch_bounds__(BLOCK) void mi_cls_kernel(KArgs a)
 	const uint32_t wave = threadIdx.x >> 6;
 	uint32_t *W = s_win + wave * WAVE * WSTRIDE;
 
-	const mi_tbl_hdr_t *hdr = (const mi_tbl_hdr_t *)a.tbl;
-	const mi_cos_t *cos_tbl = (const mi_cos_t *)(a.tbl + hdr->cos_off);
-	const mi_rule_t *rule_tbl = (const mi_rule_t *)(a.tbl + hdr->rule_off);
-	const mi_term_t *term_tbl = (const mi_term_t *)(a.tbl + hdr->term_off);
-	const int32_t def_cos = __builtin_amdgcn_readfirstlane(hdr->default_cos);
-	const int32_t err_cos = __builtin_amdgcn_readfirstlane(hdr->error_cos);
-	const uint32_t def_valid = __builtin_amdgcn_readfirstlane(hdr->default_valid);
-	const uint32_t used = __builtin_amdgcn_readfirstlane(hdr->used_kinds);
-	const uint32_t max_hops = __builtin_amdgcn_readfirstlane(hdr->max_hops);
+	const cword_t dev = (cword_t)a.dev;
+	const int32_t def_cos = (int32_t)dev[DH_DEFAULT];
+	const int32_t err_cos = (int32_t)dev[DH_ERROR];
+	const uint32_t def_valid = dev[DH_DEFAULT_VALID];
+	const uint32_t used = dev[DH_USED];
+	const uint32_t max_hops = dev[DH_MAX_HOPS];
+	const cword_t cos_tbl = dev + dev[DH_COS_OFF];
+	const cword_t prog = dev + dev[DH_PROG_OFF];
 	const bool stats_on = a.stats != nullptr;
 
 	if (stats_on) {
 		for (uint32_t i = threadIdx.x; i < MAX_STATS_COS; i += BLOCK)
 			s_cnt[i] = 0;
+		__syncthreads();
 	}
 
-	for (uint32_t bt = blockIdx.x; (uint64_t)bt * BLOCK < a.n; bt += gridDim.x) {
-		const uint32_t base = bt * BLOCK + wave * WAVE;
-		const uint32_t pi = base + lane;
+	const uint32_t nt = (a.n + WAVE - 1) / WAVE;
+	for (uint32_t tile = blockIdx.x * WAVES_PER_BLOCK + wave; tile < nt;
+	     tile += gridDim.x * WAVES_PER_BLOCK) {
+		const uint32_t pi = tile * WAVE + lane;
 		const bool valid = pi < a.n;
 		const uint32_t my_off = valid ? a.off[pi] : 0u;
 		const uint32_t my_len = valid ? (uint32_t)a.len[pi] : 0u;
 
-		__syncthreads();   // previous tile's windows fully consumed
-		// ---- stage the first WIN bytes of the wave's 64 packets into LDS
+		// ---- stage the first WIN bytes of the wave's 64 packets into LDS.
+		// Phase 1 issues every 16-B load before any is consumed (one HBM
+		// round trip per tile, not eight).
+		uint32_t q_off[8], q_len[8];
+		uint4 d[8];
 #pragma unroll
 		for (uint32_t r = 0; r < 8; ++r) {
 			const uint32_t q = r * 8u + (lane >> 3);
-			const uint32_t c = lane & 7u;
-			const uint32_t q_off = __shfl(my_off, (int)q);
-			const uint32_t q_len = __shfl(my_len, (int)q);
-			const uint32_t b0 = c * 16u;
-			uint4 d = make_uint4(0, 0, 0, 0);
-			if (b0 < q_len) {
-				const uint8_t *src = a.pkts + q_off + b0;
-				if ((q_off & 15u) == 0u) {
-					d = *(const uint4 *)src;
-				} else {
-					uint32_t t[4];
+			q_off[r] = __shfl(my_off, (int)q);
+			q_len[r] = __shfl(my_len, (int)q);
+		}
 #pragma unroll
-					for (int i = 0; i < 4; ++i)
-						t[i] = (uint32_t)src[4 * i] | ((uint32_t)src[4 * i + 1] << 8) |
-						       ((uint32_t)src[4 * i + 2] << 16) | ((uint32_t)src[4 * i + 3] << 24);
-					d = make_uint4(t[0], t[1], t[2], t[3]);
-				}
-				const uint32_t rem = q_len - b0;   // bytes of the piece inside the frame
+		for (uint32_t r = 0; r < 8; ++r) {
+			const uint32_t b0 = (lane & 7u) * 16u;
+			d[r] = make_uint4(0, 0, 0, 0);
+			// gfx950 global loads tolerate any alignment; 16-B aligned frames
+			// (the batch layout's contract) take the full-rate path
+			if (b0 < q_len[r])
+				__builtin_memcpy(&d[r], a.pkts + q_off[r] + b0, 16);
+		}
+		wave_lds_sync();   // previous tile's window reads are done
+#pragma unroll
+		for (uint32_t r = 0; r < 8; ++r) {
+			const uint32_t q = r * 8u + (lane >> 3);
+			const uint32_t b0 = (lane & 7u) * 16u;
+			uint32_t t[4] = { d[r].x, d[r].y, d[r].z, d[r].w };
+			if (b0 < q_len[r]) {
+				const uint32_t rem = q_len[r] - b0;   // frame bytes in this piece
 				if (rem < 16u) {
-					uint32_t t[4] = { d.x, d.y, d.z, d.w };
 #pragma unroll
 					for (uint32_t i = 0; i < 4; ++i) {
-						uint32_t lo = 4u * i;
-						uint32_t keep = rem <= lo ? 0u : (rem >= lo + 4u ? 0xffffffffu
-								: (0xffffffffu >> (8u * (lo + 4u - rem))));
+						const uint32_t lo = 4u * i;
+						const uint32_t keep = rem <= lo ? 0u : (rem >= lo + 4u ? 0xffffffffu
+							: (0xffffffffu >> (8u * (lo + 4u - rem))));
 						t[i] &= keep;
 					}
-					d = make_uint4(t[0], t[1], t[2], t[3]);
 				}
 			}
-			uint32_t *dst = W + q * WSTRIDE + c * 4u;
-			dst[0] = d.x;
-			dst[1] = d.y;
-			dst[2] = d.z;
-			dst[3] = d.w;
+			uint32_t *dst = W + q * WSTRIDE + (lane & 7u) * 4u;
+			dst[0] = t[0];
+			dst[1] = t[1];
+			dst[2] = t[2];
+			dst[3] = t[3];
 		}
 		W[lane * WSTRIDE + 32] = 0u;
-		__syncthreads();
+		wave_lds_sync();
 
 		Pkt k;
 		k.w = W + lane * WSTRIDE;
@@ -647,27 +815,96 @@ __global__ __launch_bounds__(BLOCK) void mi_cls_kernel(KArgs a)
 				break;
 			const int32_t c = __builtin_amdgcn_readlane(cur, (int)__builtin_ctzll(pm));
 			const bool in_grp = pend && cur == c;
-			const mi_cos_t *cd = cos_tbl + c;
-			const uint32_t rb0 = __builtin_amdgcn_readfirstlane(cd->rule_begin);
-			const uint32_t nr = __builtin_amdgcn_readfirstlane(cd->num_rules);
+			const uint32_t rec0 = cos_tbl[COS_WORDS * (uint32_t)c];
+			const uint32_t nr = cos_tbl[COS_WORDS * (uint32_t)c + 1u];
+			const uint32_t bv = cos_tbl[COS_WORDS * (uint32_t)c + 4u];
 			bool done = false;
 			uint32_t nxt = 0, nmark = 0;
-			for (uint32_t r = 0; r < nr; ++r) {
+			if (bv != 0u && nr != 0u) {
+				// ---- bit-vector path: one hash probe + row gathers per class
+				const cword_t blk = dev + bv;
+				const uint32_t Wd = blk[0], ncls = blk[1], alive = blk[2];
+				uint32_t ridx[BV_MAX_CLS];
+#pragma unroll
+				for (uint32_t kc = 0; kc < BV_MAX_CLS; ++kc) {
+					ridx[kc] = 0;
+					if (kc < ncls) {
+						const cword_t cr = blk + 4u + BV_CLS_WORDS * kc;
+						const uint32_t nk = cr[1], tmask = cr[9], tbl = cr[10], rows = cr[11];
+						uint32_t key[4];
+						const bool present = bv_key(cr, k, p, x, key);
+						uint32_t row = 0;
+						if (in_grp && present) {
+							uint32_t h = bv_hash(key) & tmask;
+							for (uint32_t probe = 0; probe <= tmask; ++probe) {
+								const uint32_t *sl = a.dev + tbl + h * (nk + 1u);
+								const uint32_t rw = sl[nk];
+								if (rw == BV_EMPTY)
+									break;
+								bool eq = sl[0] == key[0];
+								if (nk > 1)
+									eq = eq && sl[1] == key[1];
+								if (nk > 2)
+									eq = eq && sl[2] == key[2] && sl[3] == key[3];
+								if (eq) {
+									row = rw;
+									break;
+								}
+								h = (h + 1u) & tmask;
+							}
+						}
+						ridx[kc] = rows + row * Wd;
+					}
+				}
+				uint32_t first = 0;
+				for (uint32_t w = 0; w < Wd; ++w) {
+					if (__ballot(in_grp && !done) == 0ull)
+						break;
+					if (in_grp && !done) {
+						uint32_t acc = dev[alive + w];
+#pragma unroll
+						for (uint32_t kc = 0; kc < BV_MAX_CLS; ++kc)
+							if (kc < ncls)
+								acc &= a.dev[ridx[kc] + w];
+						if (acc) {
+							done = true;
+							first = w * 32u + (uint32_t)__builtin_ctz(acc);
+						}
+					}
+				}
+				if (in_grp && done) {
+					const uint32_t *rec = a.dev + dev[DH_PROG_OFF] + (rec0 + first) * REC_WORDS;
+					nxt = rec[1] & 0xffu;
+					nmark = rec[0] >> 16;
+				}
+			}
+			for (uint32_t r = 0; r < nr && bv == 0u; ++r) {
 				const bool cand = in_grp && !done;
 				if (__ballot(cand) == 0ull)
 					break;
-				const mi_rule_t *ru = rule_tbl + rb0 + r;
-				const uint32_t tb = __builtin_amdgcn_readfirstlane(ru->term_begin);
-				const uint32_t nt = __builtin_amdgcn_readfirstlane(ru->num_terms);
+				const uint32_t base = (rec0 + r) * REC_WORDS;
+				const uint32_t w0 = prog[base];
+				const uint32_t w1 = prog[base + 1];
+				const uint32_t n_in = w0 & 0xfu, n_ext = (w0 >> 8) & 0xfu;
+				// AND of the terms; stop as soon as no lane can still match
 				bool ok = cand;
-				for (uint32_t t = 0; t < nt; ++t) {
+				uint32_t q = base + 2;
+				for (uint32_t t = 0; t < n_in; ++t) {
 					if (__ballot(ok) == 0ull)
 						break;
-					ok = ok && term_ok(term_tbl + tb + t, k, p, x);
+					ok = term_ok(prog, q, k, p, x) && ok;
+				}
+				if (n_ext && __ballot(ok) != 0ull) {
+					q = w1 >> 8;
+					for (uint32_t t = 0; t < n_ext; ++t) {
+						if (__ballot(ok) == 0ull)
+							break;
+						ok = term_ok(prog, q, k, p, x) && ok;
+					}
 				}
 				if (ok) {
-					nxt = __builtin_amdgcn_readfirstlane(ru->dst_cos);
-					nmark = __builtin_amdgcn_readfirstlane(ru->mark);
+					nxt = w1 & 0xffu;
+					nmark = w0 >> 16;
 					done = true;
 				}
 			}
@@ -717,15 +954,16 @@ __global__ __launch_bounds__(BLOCK) void mi_cls_kernel(KArgs a)
 			if (fc < 0) {
 				outcome = MI_CLS_OUT_DISCARD;
 			} else {
-				const mi_cos_t cdesc = cos_tbl[fc];
-				cos_idx = cdesc.index;
-				if (cdesc.action == 1u) {
+				const uint32_t meta = a.dev[dev[DH_COS_OFF] + COS_WORDS * (uint32_t)fc + 2u];
+				cos_idx = meta >> 24;
+				const uint32_t nq = (meta >> 8) & 0xffu;
+				if (meta & 0xffu) {
 					outcome = MI_CLS_OUT_COS_DROP;
 				} else {
 					outcome = MI_CLS_OUT_ENQ;
-					if (cdesc.num_queue > 1u) {
-						uint32_t h = rss_hash(k, p, cdesc.hash_proto) & 31u;
-						queue = h % cdesc.num_queue;
+					if (nq > 1u) {
+						uint32_t h = rss_hash(k, p, (meta >> 16) & 0xffu) & 31u;
+						queue = h % nq;
 					}
 				}
 			}
@@ -753,9 +991,8 @@ __global__ __launch_bounds__(BLOCK) void mi_cls_kernel(KArgs a)
 // ------------------------------------------------------------------- host
 struct mi_cls_ctx {
 	int device;
-	uint8_t *d_tbl;
-	size_t tbl_cap;
-	size_t tbl_bytes;
+	uint32_t *d_dev;         // assembled device rule program
+	size_t dev_cap;          // bytes
 	int loaded;
 	unsigned long long *d_stats;
 	int stats_on;
@@ -811,8 +1048,8 @@ extern "C" int mi_cls_ctx_destroy(mi_cls_ctx_t *c)
 	if (!c)
 		return -EINVAL;
 	(void)hipSetDevice(c->device);
-	if (c->d_tbl)
-		(void)hipFree(c->d_tbl);
+	if (c->d_dev)
+		(void)hipFree(c->d_dev);
 	if (c->d_stats)
 		(void)hipFree(c->d_stats);
 	free(c);
@@ -858,6 +1095,262 @@ static int validate_tbl(const void *tbl, size_t bytes)
 	return 0;
 }
 
+// words of one term in the device encoding (see "device rule program")
+static uint32_t encode_term(const mi_term_t &t, uint32_t *w)
+{
+	uint32_t n = 0;
+	if (t.kind == MI_K_CUSTOM_FRAME || t.kind == MI_K_CUSTOM_L3) {
+		uint32_t nw = (t.size + 3u) / 4u;
+		w[n++] = t.kind | ((uint32_t)t.size << 8) | (nw << 16);
+		w[n++] = t.offset;
+		for (uint32_t i = 0; i < nw; ++i) {
+			w[n++] = t.mask[i];
+			w[n++] = t.value[i];
+		}
+		return n;
+	}
+	uint32_t nw = (t.kind == MI_K_SIP6 || t.kind == MI_K_DIP6) ? 4u : (t.kind == MI_K_DMAC ? 2u : 1u);
+	w[n++] = t.kind | ((uint32_t)t.size << 8) | (nw << 16);
+	for (uint32_t i = 0; i < nw; ++i) {
+		w[n++] = t.mask[i];
+		w[n++] = t.value[i];
+	}
+	return n;
+}
+
+// ---- bit-vector block construction (host) ----
+struct ClassKey {
+	uint32_t kind, nkey, offset, size, mask[4];
+	bool operator<(const ClassKey &o) const
+	{
+		if (kind != o.kind) return kind < o.kind;
+		if (offset != o.offset) return offset < o.offset;
+		if (size != o.size) return size < o.size;
+		for (int i = 0; i < 4; ++i)
+			if (mask[i] != o.mask[i]) return mask[i] < o.mask[i];
+		return false;
+	}
+};
+
+typedef std::array<uint32_t, 4> Key4;
+
+static uint32_t host_bv_hash(const Key4 &k)
+{
+	uint32_t h = k[0] * 0x9E3779B1u ^ k[1] * 0x85EBCA77u ^ k[2] * 0xC2B2AE3Du ^ k[3] * 0x27D4EB2Fu;
+	h ^= h >> 15;
+	h *= 0x2C1B3C6Du;
+	h ^= h >> 12;
+	return h;
+}
+
+static bool class_of(const mi_term_t &t, ClassKey &ck)
+{
+	memset(&ck, 0, sizeof(ck));
+	ck.kind = t.kind;
+	switch (t.kind) {
+	case MI_K_NEVER:
+	case MI_K_ALWAYS:
+		return false;
+	case MI_K_CUSTOM_FRAME:
+	case MI_K_CUSTOM_L3:
+		ck.offset = t.offset;
+		ck.size = t.size;
+		ck.nkey = t.size > 8 ? 4 : (t.size > 4 ? 2 : 1);
+		break;
+	case MI_K_SIP6:
+	case MI_K_DIP6:
+		ck.nkey = 4;
+		break;
+	case MI_K_DMAC:
+		ck.nkey = 2;
+		break;
+	default:
+		ck.nkey = 1;
+	}
+	for (uint32_t i = 0; i < 4; ++i)
+		ck.mask[i] = i < ck.nkey ? t.mask[i] : 0;
+	return true;
+}
+
+// Build the BV block of one CoS into `blk` (word offsets relative to the
+// start of the device program, base = blk's first word index).  Returns false
+// when the CoS needs more than BV_MAX_CLS classes (linear scan instead).
+static bool build_bv(const mi_rule_t *rs, const mi_term_t *ts, uint32_t nrules, uint32_t base,
+		     std::vector<uint32_t> &blk)
+{
+	std::map<ClassKey, uint32_t> cls;
+	std::vector<ClassKey> cls_list;
+	for (uint32_t r = 0; r < nrules; ++r)
+		for (uint32_t t = 0; t < rs[r].num_terms; ++t) {
+			ClassKey ck;
+			if (class_of(ts[rs[r].term_begin + t], ck) && !cls.count(ck)) {
+				cls[ck] = (uint32_t)cls_list.size();
+				cls_list.push_back(ck);
+			}
+		}
+	const uint32_t ncls = (uint32_t)cls_list.size();
+	if (ncls > BV_MAX_CLS)
+		return false;
+	const uint32_t W = (nrules + 31u) / 32u;
+	// per rule: alive bit, and per class the required key (or none)
+	std::vector<uint32_t> alive(W, 0);
+	std::vector<std::map<Key4, std::vector<uint32_t>>> rows_of(ncls);   // key -> rule list
+	std::vector<std::vector<uint32_t>> dc(ncls, std::vector<uint32_t>(W, 0));
+	for (uint32_t r = 0; r < nrules; ++r) {
+		bool ok = true;
+		std::vector<int> have(ncls, 0);
+		std::vector<Key4> want(ncls);
+		for (uint32_t t = 0; t < rs[r].num_terms; ++t) {
+			const mi_term_t &tm = ts[rs[r].term_begin + t];
+			ClassKey ck;
+			if (!class_of(tm, ck)) {
+				if (tm.kind == MI_K_NEVER)
+					ok = false;
+				continue;
+			}
+			uint32_t c = cls[ck];
+			Key4 v = { 0, 0, 0, 0 };
+			for (uint32_t i = 0; i < ck.nkey; ++i)
+				v[i] = tm.value[i];
+			if (have[c] && want[c] != v)
+				ok = false;   // two terms of one class with different values
+			have[c] = 1;
+			want[c] = v;
+		}
+		if (!ok)
+			continue;
+		alive[r >> 5] |= 1u << (r & 31);
+		for (uint32_t c = 0; c < ncls; ++c) {
+			if (have[c])
+				rows_of[c][want[c]].push_back(r);
+			else
+				dc[c][r >> 5] |= 1u << (r & 31);
+		}
+	}
+	// layout: header (4) | classes (16 each) | alive row | per class: table, rows
+	blk.assign(4 + BV_CLS_WORDS * ncls, 0);
+	blk[0] = W;
+	blk[1] = ncls;
+	blk[2] = base + (uint32_t)blk.size();
+	blk.insert(blk.end(), alive.begin(), alive.end());
+	for (uint32_t c = 0; c < ncls; ++c) {
+		const ClassKey &ck = cls_list[c];
+		const uint32_t nvals = (uint32_t)rows_of[c].size();
+		uint32_t tsize = 4;
+		while (tsize < 2 * (nvals + 1))
+			tsize <<= 1;
+		uint32_t *cr = &blk[4 + BV_CLS_WORDS * c];
+		cr[0] = ck.kind;
+		cr[1] = ck.nkey;
+		cr[3] = ck.offset;
+		cr[4] = ck.size;
+		for (int i = 0; i < 4; ++i)
+			cr[5 + i] = ck.mask[i];
+		cr[9] = tsize - 1;
+		const uint32_t tbl_off = (uint32_t)blk.size();
+		cr = nullptr;
+		blk.resize(blk.size() + (size_t)tsize * (ck.nkey + 1), 0);
+		for (uint32_t i = 0; i < tsize; ++i)
+			blk[tbl_off + i * (ck.nkey + 1) + ck.nkey] = BV_EMPTY;
+		const uint32_t rows_off = (uint32_t)blk.size();
+		// row 0: rules without a term of this class
+		blk.insert(blk.end(), dc[c].begin(), dc[c].end());
+		uint32_t row = 1;
+		for (auto &kv : rows_of[c]) {
+			std::vector<uint32_t> bits = dc[c];
+			for (uint32_t r : kv.second)
+				bits[r >> 5] |= 1u << (r & 31);
+			blk.insert(blk.end(), bits.begin(), bits.end());
+			uint32_t h = host_bv_hash(kv.first) & (tsize - 1);
+			while (blk[tbl_off + h * (ck.nkey + 1) + ck.nkey] != BV_EMPTY)
+				h = (h + 1) & (tsize - 1);
+			for (uint32_t i = 0; i < ck.nkey; ++i)
+				blk[tbl_off + h * (ck.nkey + 1) + i] = kv.first[i];
+			blk[tbl_off + h * (ck.nkey + 1) + ck.nkey] = row++;
+		}
+		uint32_t *cw = &blk[4 + BV_CLS_WORDS * c];
+		cw[10] = base + tbl_off;
+		cw[11] = base + rows_off;
+	}
+	return true;
+}
+
+// Assemble the mi_cls.h table into the private device encoding.
+static int assemble(const void *tbl, uint32_t **out, size_t *out_words)
+{
+	const mi_tbl_hdr_t *h = (const mi_tbl_hdr_t *)tbl;
+	const uint8_t *b = (const uint8_t *)tbl;
+	const mi_cos_t *cs = (const mi_cos_t *)(b + h->cos_off);
+	const mi_rule_t *rs = (const mi_rule_t *)(b + h->rule_off);
+	const mi_term_t *ts = (const mi_term_t *)(b + h->term_off);
+	const uint32_t cos_off = DH_WORDS, prog_off = cos_off + COS_WORDS * h->num_cos;
+	std::vector<uint32_t> w(prog_off + (size_t)h->num_rules * REC_WORDS, 0);
+	w[DH_MAGIC] = DEV_MAGIC;
+	w[DH_NCOS] = h->num_cos;
+	w[DH_DEFAULT] = (uint32_t)h->default_cos;
+	w[DH_ERROR] = (uint32_t)h->error_cos;
+	w[DH_DEFAULT_VALID] = h->default_valid;
+	w[DH_USED] = h->used_kinds;
+	w[DH_MAX_HOPS] = h->max_hops;
+	w[DH_COS_OFF] = cos_off;
+	w[DH_PROG_OFF] = prog_off;
+	for (uint32_t s = 0; s < h->num_cos; ++s) {
+		uint32_t *c = &w[cos_off + COS_WORDS * s];
+		c[0] = cs[s].rule_begin;
+		c[1] = cs[s].num_rules;
+		c[2] = (uint32_t)cs[s].action | ((uint32_t)cs[s].num_queue << 8) |
+		       ((uint32_t)cs[s].hash_proto << 16) | ((uint32_t)cs[s].index << 24);
+		c[3] = cs[s].valid;
+	}
+	// 16-word rule records (+ ext terms appended after them)
+	std::vector<uint32_t> ext;
+	const size_t ext_base = (size_t)h->num_rules * REC_WORDS;
+	for (uint32_t r = 0; r < h->num_rules; ++r) {
+		uint32_t *rec = &w[prog_off + (size_t)r * REC_WORDS];
+		uint32_t used = 2, n_in = 0, n_ext = 0;
+		size_t ext_begin = ext_base + ext.size();
+		for (uint32_t t = 0; t < rs[r].num_terms; ++t) {
+			uint32_t tw[12];
+			uint32_t n = encode_term(ts[rs[r].term_begin + t], tw);
+			if (n_ext == 0 && used + n <= REC_WORDS) {
+				memcpy(rec + used, tw, n * sizeof(uint32_t));
+				used += n;
+				n_in++;
+			} else {
+				ext.insert(ext.end(), tw, tw + n);
+				n_ext++;
+			}
+		}
+		if (ext_begin >= (1u << 24))
+			return -E2BIG;
+		rec[0] = n_in | (n_ext << 8) | ((uint32_t)rs[r].mark << 16);
+		rec[1] = rs[r].dst_cos | ((uint32_t)(n_ext ? ext_begin : 0) << 8);
+	}
+	w.insert(w.end(), ext.begin(), ext.end());
+	// bit-vector blocks (absolute word offsets)
+	if (!getenv("MI_CLS_NO_BV")) {
+		for (uint32_t s = 0; s < h->num_cos; ++s) {
+			if (!cs[s].valid || cs[s].num_rules == 0)
+				continue;
+			std::vector<uint32_t> blk;
+			const uint32_t base = (uint32_t)w.size();
+			if (build_bv(rs + cs[s].rule_begin, ts, cs[s].num_rules, base, blk)) {
+				w[cos_off + COS_WORDS * s + 4] = base;
+				w.insert(w.end(), blk.begin(), blk.end());
+			}
+		}
+	}
+	w.resize(w.size() + 16, 0);
+	w[DH_TOTAL] = (uint32_t)w.size();
+	uint32_t *o = (uint32_t *)malloc(w.size() * sizeof(uint32_t));
+	if (!o)
+		return -ENOMEM;
+	memcpy(o, w.data(), w.size() * sizeof(uint32_t));
+	*out = o;
+	*out_words = w.size();
+	return 0;
+}
+
 extern "C" int mi_cls_rules_load(mi_cls_ctx_t *c, const void *tbl, size_t bytes, void *stream)
 {
 	if (!c)
@@ -865,22 +1358,35 @@ extern "C" int mi_cls_rules_load(mi_cls_ctx_t *c, const void *tbl, size_t bytes,
 	int rc = validate_tbl(tbl, bytes);
 	if (rc)
 		return rc;
-	HIP_OK(hipSetDevice(c->device));
-	if (bytes > c->tbl_cap) {
-		// stream-ordered free of the old table: wait for in-flight work first
-		if (c->d_tbl) {
-			HIP_OK(hipStreamSynchronize((hipStream_t)stream));
-			(void)hipFree(c->d_tbl);
-			c->d_tbl = nullptr;
+	uint32_t *w = nullptr;
+	size_t words = 0;
+	rc = assemble(tbl, &w, &words);
+	if (rc)
+		return rc;
+	size_t nbytes = words * sizeof(uint32_t);
+	if (hipSetDevice(c->device) != hipSuccess)
+		return free(w), -EIO;
+	if (nbytes > c->dev_cap) {
+		// the old program may still be read by in-flight launches
+		if (c->d_dev) {
+			if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess)
+				return free(w), -EIO;
+			(void)hipFree(c->d_dev);
+			c->d_dev = nullptr;
 		}
-		size_t cap = bytes < 4096 ? 4096 : bytes;
-		HIP_OK(hipMalloc((void **)&c->d_tbl, cap));
-		c->tbl_cap = cap;
+		size_t cap = nbytes < 4096 ? 4096 : nbytes;
+		if (hipMalloc((void **)&c->d_dev, cap) != hipSuccess)
+			return free(w), -ENOMEM;
+		c->dev_cap = cap;
 	}
-	// the blob lives in caller memory that may be freed right after return
-	HIP_OK(hipMemcpyAsync(c->d_tbl, tbl, bytes, hipMemcpyHostToDevice, (hipStream_t)stream));
-	HIP_OK(hipStreamSynchronize((hipStream_t)stream));
-	c->tbl_bytes = bytes;
+	// stream-ordered after earlier launches; synchronous w.r.t. the host
+	// buffer, which is freed on return
+	hipError_t e = hipMemcpyAsync(c->d_dev, w, nbytes, hipMemcpyHostToDevice, (hipStream_t)stream);
+	if (e == hipSuccess)
+		e = hipStreamSynchronize((hipStream_t)stream);
+	free(w);
+	if (e != hipSuccess)
+		return -EIO;
 	c->loaded = 1;
 	return 0;
 }
@@ -902,12 +1408,12 @@ extern "C" int mi_cls_classify(mi_cls_ctx_t *c, const uint8_t *pkts, const uint3
 	a.off = off;
 	a.len = len;
 	a.n = n;
-	a.tbl = c->d_tbl;
+	a.dev = c->d_dev;
 	a.out = out;
 	a.stats = c->stats_on ? c->d_stats : nullptr;
 	memcpy(a.stats_mask, c->stats_mask, sizeof(a.stats_mask));
 	uint32_t tiles = (n + BLOCK - 1) / BLOCK;
-	uint32_t max_grid = (uint32_t)c->num_cu * 16u;
+	uint32_t max_grid = (uint32_t)c->num_cu * 8u;
 	uint32_t grid = tiles < max_grid ? tiles : max_grid;
 	hipLaunchKernelGGL(mi_cls_kernel, dim3(grid), dim3(BLOCK), 0, (hipStream_t)stream, a);
 	if (hipGetLastError() != hipSuccess)

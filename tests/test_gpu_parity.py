@@ -16,10 +16,21 @@ from tests.helpers import assert_same, gpu_run, oracle_run, summary
 pytestmark = pytest.mark.gpu
 
 
-def both(prog, batch, limits=(255, 8192, 4096), what=""):
-    got = gpu_run(prog, batch, limits)
+def both(prog, batch, limits=(255, 8192, 4096), what="", engine="auto"):
+    """engine "auto": bit-vector blocks where a CoS has <= 8 key classes,
+    linear scan otherwise; "linear": force the linear scan everywhere."""
+    import os
+    old = os.environ.pop("MI_CLS_NO_BV", None)
+    if engine == "linear":
+        os.environ["MI_CLS_NO_BV"] = "1"
+    try:
+        got = gpu_run(prog, batch, limits)
+    finally:
+        os.environ.pop("MI_CLS_NO_BV", None)
+        if old is not None:
+            os.environ["MI_CLS_NO_BV"] = old
     exp, _ = oracle_run(prog, batch, limits)
-    assert_same(got, exp, batch, what)
+    assert_same(got, exp, batch, f"{what} [{engine}]")
     return got
 
 
@@ -38,10 +49,11 @@ def test_zoo_no_rules(built, gpu):
     both([R.cos("d", queue=1), ("default", 0)], b, what="zoo/no rules")
 
 
+@pytest.mark.parametrize("engine", ["auto", "linear"])
 @pytest.mark.parametrize("name,term", zoo.term_examples(), ids=[n for n, _ in zoo.term_examples()])
-def test_zoo_each_term(built, gpu, name, term):
+def test_zoo_each_term(built, gpu, name, term, engine):
     b, names = zoo.zoo_batch()
-    got = both(zoo.prog_single(term, mark=7), b, what=name)
+    got = both(zoo.prog_single(term, mark=7), b, what=name, engine=engine)
     assert got.shape[0] == len(names)
 
 
@@ -70,22 +82,25 @@ def test_zoo_no_default(built, gpu):
     assert s["discard"] > 0 and s["cos_drop"] > 0
 
 
+@pytest.mark.parametrize("engine", ["auto", "linear"])
 @pytest.mark.parametrize("seed", range(12))
-def test_random_programs_fuzz(built, gpu, seed):
+def test_random_programs_fuzz(built, gpu, seed, engine):
     rng = np.random.default_rng(1000 + seed)
     frames = [f for _, f in zoo.all_frames()]
     fr = frames + zoo.mutate_frames(rng, frames, 3000)
     b = pg.batch_from_frames(fr)
     prog = zoo.random_program(rng, frames, n_cos=int(rng.integers(3, 40)),
-                              n_rules=int(rng.integers(5, 200)))
-    both(prog, b, what=f"fuzz seed {seed}")
+                              n_rules=int(rng.integers(5, 200)),
+                              max_kinds=None if seed % 2 else 6)
+    both(prog, b, what=f"fuzz seed {seed}", engine=engine)
 
 
+@pytest.mark.parametrize("engine", ["auto", "linear"])
 @pytest.mark.parametrize("cfg,n", [(1, 10_000), (2, 100_000), (3, 50_000), (4, 50_000),
                                    (5, 20_000)])
-def test_configs_small(built, gpu, cfg, n):
+def test_configs_small(built, gpu, cfg, n, engine):
     b, prog = R.CONFIGS[cfg](n)
-    got = both(prog, b, what=f"config {cfg}")
+    got = both(prog, b, what=f"config {cfg}", engine=engine)
     assert summary(got)["enq"] > 0
 
 

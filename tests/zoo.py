@@ -277,10 +277,14 @@ def prog_no_default():
     return [R.cos("a", queue=1), R.cos("err", action=1), ("error", 1)]
 
 
-def random_program(rng, frames, n_cos=12, n_rules=60, with_deletes=True):
+def random_program(rng, frames, n_cos=12, n_rules=60, with_deletes=True, max_kinds=None):
     """Random CoS graph with random terms whose values come from zoo frames
-    (so that they match), random masks, random marks."""
+    (so that they match), random masks, random marks.  ``max_kinds`` limits
+    the term vocabulary so that CoS lists fit the bit-vector engine."""
     ex = [t for _, t in term_examples()]
+    if max_kinds is not None:
+        idx = rng.choice(len(ex), size=max_kinds, replace=False)
+        ex = [ex[int(i)] for i in idx]
     p = [R.cos("default", queue=1)]
     for i in range(1, n_cos):
         r = rng.random()
@@ -301,7 +305,7 @@ def random_program(rng, frames, n_cos=12, n_rules=60, with_deletes=True):
         for _ in range(k):
             t = ex[int(rng.integers(0, len(ex)))]
             term, val, mask, off = t
-            if rng.random() < 0.3 and len(val):
+            if rng.random() < 0.3 and len(val) and max_kinds is None:
                 mask = bytes(int(b) & int(rng.integers(0, 256)) for b in mask)
             terms.append((term, val, mask, off))
         # mostly a DAG (src < dst) so descents terminate
