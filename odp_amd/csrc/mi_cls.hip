@@ -32,6 +32,7 @@
 
 #include "mi_cls.h"
 
+#include <algorithm>
 #include <array>
 #include <map>
 #include <vector>
@@ -672,6 +673,111 @@ __device__ __forceinline__ bool bv_key(cword_t cr, const Pkt &k, const Parsed &p
 	}
 }
 
+// Bit-vector evaluation of one CoS for the lanes in `act`.  `blk` is the
+// CoS's BV block and `rec` its first rule record; both may be wave-uniform
+// (scalar loads) or per lane (gathers), decided per call site after inlining.
+// On return, lanes of `act` with a matching rule have done = true and the
+// rule's destination CoS / mark in nxt / nmark.
+__device__ __forceinline__ void bv_eval(cword_t blk, const uint32_t *rec, bool act, const Pkt &k,
+					const Parsed &p, const Fields &x, const uint32_t *dv,
+					bool &done, uint32_t &nxt, uint32_t &nmark)
+{
+	const uint32_t Wd = blk[0], ncls = blk[1], alive = blk[2];
+	uint32_t ridx[BV_MAX_CLS];
+#pragma unroll
+	for (uint32_t kc = 0; kc < BV_MAX_CLS; ++kc) {
+		ridx[kc] = 0;
+		if (kc < ncls) {
+			const cword_t cr = blk + 4u + BV_CLS_WORDS * kc;
+			const uint32_t nk = cr[1], tmask = cr[9], tbl = cr[10], rows = cr[11];
+			uint32_t key[4];
+			const bool present = bv_key(cr, k, p, x, key);
+			uint32_t row = 0;
+			if (act && present) {
+				uint32_t h = bv_hash(key) & tmask;
+				for (uint32_t probe = 0; probe <= tmask; ++probe) {
+					const uint32_t *sl = dv + tbl + h * (nk + 1u);
+					const uint32_t rw = sl[nk];
+					if (rw == BV_EMPTY)
+						break;
+					bool eq = sl[0] == key[0];
+					if (nk > 1)
+						eq = eq && sl[1] == key[1];
+					if (nk > 2)
+						eq = eq && sl[2] == key[2] && sl[3] == key[3];
+					if (eq) {
+						row = rw;
+						break;
+					}
+					h = (h + 1u) & tmask;
+				}
+			}
+			ridx[kc] = rows + row * Wd;
+		}
+	}
+	uint32_t first = 0;
+	bool found = false;
+	for (uint32_t w = 0; w < Wd; ++w) {
+		if (__ballot(act && !found) == 0ull)
+			break;
+		if (act && !found) {
+			uint32_t acc = dv[alive + w];
+#pragma unroll
+			for (uint32_t kc = 0; kc < BV_MAX_CLS; ++kc)
+				if (kc < ncls)
+					acc &= dv[ridx[kc] + w];
+			if (acc) {
+				found = true;
+				first = w * 32u + (uint32_t)__builtin_ctz(acc);
+			}
+		}
+	}
+	if (act && found) {
+		const uint32_t *r = rec + first * REC_WORDS;
+		nxt = r[1] & 0xffu;
+		nmark = r[0] >> 16;
+		done = true;
+	}
+}
+
+// Linear scan of one wave-uniform CoS's rule records for the lanes in
+// `grp` (verify_pmr over cos->pmr[] in order, first match wins).
+__device__ __forceinline__ void linear_scan(cword_t prog, uint32_t rec0, uint32_t nr, bool grp,
+					    const Pkt &k, const Parsed &p, const Fields &x,
+					    bool &done, uint32_t &nxt, uint32_t &nmark)
+{
+	for (uint32_t r = 0; r < nr; ++r) {
+		const bool cand = grp && !done;
+		if (__ballot(cand) == 0ull)
+			break;
+		const uint32_t base = (rec0 + r) * REC_WORDS;
+		const uint32_t w0 = prog[base];
+		const uint32_t w1 = prog[base + 1];
+		const uint32_t n_in = w0 & 0xfu, n_ext = (w0 >> 8) & 0xfu;
+		// AND of the terms; stop as soon as no lane can still match
+		bool ok = cand;
+		uint32_t q = base + 2;
+		for (uint32_t t = 0; t < n_in; ++t) {
+			if (__ballot(ok) == 0ull)
+				break;
+			ok = term_ok(prog, q, k, p, x) && ok;
+		}
+		if (n_ext && __ballot(ok) != 0ull) {
+			q = w1 >> 8;
+			for (uint32_t t = 0; t < n_ext; ++t) {
+				if (__ballot(ok) == 0ull)
+					break;
+				ok = term_ok(prog, q, k, p, x) && ok;
+			}
+		}
+		if (ok) {
+			nxt = w1 & 0xffu;
+			nmark = w0 >> 16;
+			done = true;
+		}
+	}
+}
+
 // ------------------------------------------------------------------ kernel
 struct KArgs {
 	const uint8_t *pkts;
@@ -806,109 +912,62 @@ __global__ __launch_bounds__(BLOCK) void mi_cls_kernel(KArgs a)
 		if (__ballot(pend))
 			load_fields(k, p, used, x);
 
-		// ---- CoS descent as a wavefront waterfall (match_pmr_cos, :1624-1667)
+		// ---- CoS descent (match_pmr_cos, :1624-1667).  Each round moves every
+		// pending lane one hop: lanes on a bit-vector CoS evaluate it in
+		// parallel (uniformly when they all sit on one CoS -- scalar loads --
+		// or each on its own CoS); lanes on a linear-scan CoS are served one
+		// CoS per round, wave-uniform, with the rule words in SGPRs.
 		uint32_t hops = 0, mark = 0;
 		bool matched = false, loop = false;
 		for (;;) {
 			const unsigned long long pm = __ballot(pend);
 			if (pm == 0ull)
 				break;
-			const int32_t c = __builtin_amdgcn_readlane(cur, (int)__builtin_ctzll(pm));
-			const bool in_grp = pend && cur == c;
-			const uint32_t rec0 = cos_tbl[COS_WORDS * (uint32_t)c];
-			const uint32_t nr = cos_tbl[COS_WORDS * (uint32_t)c + 1u];
-			const uint32_t bv = cos_tbl[COS_WORDS * (uint32_t)c + 4u];
-			bool done = false;
+			const int32_t c0 = __builtin_amdgcn_readlane(cur, (int)__builtin_ctzll(pm));
+			const bool uniform = __ballot(pend && cur != c0) == 0ull;
+			bool done = false, proc = false;
 			uint32_t nxt = 0, nmark = 0;
-			if (bv != 0u && nr != 0u) {
-				// ---- bit-vector path: one hash probe + row gathers per class
-				const cword_t blk = dev + bv;
-				const uint32_t Wd = blk[0], ncls = blk[1], alive = blk[2];
-				uint32_t ridx[BV_MAX_CLS];
-#pragma unroll
-				for (uint32_t kc = 0; kc < BV_MAX_CLS; ++kc) {
-					ridx[kc] = 0;
-					if (kc < ncls) {
-						const cword_t cr = blk + 4u + BV_CLS_WORDS * kc;
-						const uint32_t nk = cr[1], tmask = cr[9], tbl = cr[10], rows = cr[11];
-						uint32_t key[4];
-						const bool present = bv_key(cr, k, p, x, key);
-						uint32_t row = 0;
-						if (in_grp && present) {
-							uint32_t h = bv_hash(key) & tmask;
-							for (uint32_t probe = 0; probe <= tmask; ++probe) {
-								const uint32_t *sl = a.dev + tbl + h * (nk + 1u);
-								const uint32_t rw = sl[nk];
-								if (rw == BV_EMPTY)
-									break;
-								bool eq = sl[0] == key[0];
-								if (nk > 1)
-									eq = eq && sl[1] == key[1];
-								if (nk > 2)
-									eq = eq && sl[2] == key[2] && sl[3] == key[3];
-								if (eq) {
-									row = rw;
-									break;
-								}
-								h = (h + 1u) & tmask;
-							}
-						}
-						ridx[kc] = rows + row * Wd;
+			if (uniform) {
+				const uint32_t rec0 = cos_tbl[COS_WORDS * (uint32_t)c0];
+				const uint32_t nr = cos_tbl[COS_WORDS * (uint32_t)c0 + 1u];
+				const uint32_t bv = cos_tbl[COS_WORDS * (uint32_t)c0 + 4u];
+				proc = pend;
+				if (bv != 0u && nr != 0u)
+					bv_eval(dev + bv, a.dev + dev[DH_PROG_OFF] + rec0 * REC_WORDS, pend, k,
+						p, x, a.dev, done, nxt, nmark);
+				else
+					linear_scan(prog, rec0, nr, pend, k, p, x, done, nxt, nmark);
+			} else {
+				const uint32_t ci = COS_WORDS * (uint32_t)(pend ? cur : c0);
+				const uint32_t my_rec0 = a.dev[dev[DH_COS_OFF] + ci];
+				const uint32_t my_nr = a.dev[dev[DH_COS_OFF] + ci + 1u];
+				const uint32_t my_bv = a.dev[dev[DH_COS_OFF] + ci + 4u];
+				const bool empty = pend && my_nr == 0u;
+				const bool bvl = pend && my_nr != 0u && my_bv != 0u;
+				if (__ballot(bvl))
+					bv_eval((cword_t)(a.dev + my_bv),
+						a.dev + dev[DH_PROG_OFF] + my_rec0 * REC_WORDS, bvl, k, p, x,
+						a.dev, done, nxt, nmark);
+				const bool lin = pend && !empty && !bvl;
+				bool grp = false;
+				const unsigned long long lm = __ballot(lin);
+				if (lm) {
+					const int32_t c1 = __builtin_amdgcn_readlane(cur, (int)__builtin_ctzll(lm));
+					grp = lin && cur == c1;
+					const uint32_t rec1 = cos_tbl[COS_WORDS * (uint32_t)c1];
+					const uint32_t nr1 = cos_tbl[COS_WORDS * (uint32_t)c1 + 1u];
+					bool d1 = false;
+					uint32_t n1 = 0, m1 = 0;
+					linear_scan(prog, rec1, nr1, grp, k, p, x, d1, n1, m1);
+					if (grp) {
+						done = d1;
+						nxt = n1;
+						nmark = m1;
 					}
 				}
-				uint32_t first = 0;
-				for (uint32_t w = 0; w < Wd; ++w) {
-					if (__ballot(in_grp && !done) == 0ull)
-						break;
-					if (in_grp && !done) {
-						uint32_t acc = dev[alive + w];
-#pragma unroll
-						for (uint32_t kc = 0; kc < BV_MAX_CLS; ++kc)
-							if (kc < ncls)
-								acc &= a.dev[ridx[kc] + w];
-						if (acc) {
-							done = true;
-							first = w * 32u + (uint32_t)__builtin_ctz(acc);
-						}
-					}
-				}
-				if (in_grp && done) {
-					const uint32_t *rec = a.dev + dev[DH_PROG_OFF] + (rec0 + first) * REC_WORDS;
-					nxt = rec[1] & 0xffu;
-					nmark = rec[0] >> 16;
-				}
+				proc = bvl || empty || grp;
 			}
-			for (uint32_t r = 0; r < nr && bv == 0u; ++r) {
-				const bool cand = in_grp && !done;
-				if (__ballot(cand) == 0ull)
-					break;
-				const uint32_t base = (rec0 + r) * REC_WORDS;
-				const uint32_t w0 = prog[base];
-				const uint32_t w1 = prog[base + 1];
-				const uint32_t n_in = w0 & 0xfu, n_ext = (w0 >> 8) & 0xfu;
-				// AND of the terms; stop as soon as no lane can still match
-				bool ok = cand;
-				uint32_t q = base + 2;
-				for (uint32_t t = 0; t < n_in; ++t) {
-					if (__ballot(ok) == 0ull)
-						break;
-					ok = term_ok(prog, q, k, p, x) && ok;
-				}
-				if (n_ext && __ballot(ok) != 0ull) {
-					q = w1 >> 8;
-					for (uint32_t t = 0; t < n_ext; ++t) {
-						if (__ballot(ok) == 0ull)
-							break;
-						ok = term_ok(prog, q, k, p, x) && ok;
-					}
-				}
-				if (ok) {
-					nxt = w1 & 0xffu;
-					nmark = w0 >> 16;
-					done = true;
-				}
-			}
-			if (in_grp) {
+			if (proc) {
 				if (done) {
 					cur = (int32_t)nxt;
 					mark = nmark;
@@ -1191,6 +1250,11 @@ static bool build_bv(const mi_rule_t *rs, const mi_term_t *ts, uint32_t nrules, 
 	const uint32_t ncls = (uint32_t)cls_list.size();
 	if (ncls > BV_MAX_CLS)
 		return false;
+	// canonical class order: CoS with the same classes evaluate them in the
+	// same order, so lanes on different CoS stay convergent
+	std::sort(cls_list.begin(), cls_list.end());
+	for (uint32_t i = 0; i < ncls; ++i)
+		cls[cls_list[i]] = i;
 	const uint32_t W = (nrules + 31u) / 32u;
 	// per rule: alive bit, and per class the required key (or none)
 	std::vector<uint32_t> alive(W, 0);
