@@ -33,23 +33,31 @@ def _run(cmd):
     return r.stdout
 
 
-def build(force: bool = False) -> list[str]:
+def build(force: bool = False, out_dir: str = PKG, defines=()) -> list[str]:
+    """Build both libraries into out_dir (default: in-tree).  ``defines``
+    (e.g. ["WIN=64"]) builds a kernel variant for A/B measurement."""
     hdrs = [os.path.join(INC, h) for h in ("mi_cls.h", "odp_cls_api.h")]
     mi_src = os.path.join(SRC, "mi_cls.hip")
-    mi_so = os.path.join(PKG, "libmi_cls.so")
+    os.makedirs(out_dir, exist_ok=True)
+    mi_so = os.path.join(out_dir, "libmi_cls.so")
     odp_src = os.path.join(SRC, "odp_cls.c")
-    odp_so = os.path.join(PKG, "libodp_cls.so")
+    odp_so = os.path.join(out_dir, "libodp_cls.so")
     built = []
-    if force or _stale(mi_so, [mi_src] + hdrs):
+    if force or defines or _stale(mi_so, [mi_src] + hdrs):
         _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-              "-Wall", "-I", INC, "-o", mi_so, mi_src])
+              "-Wall", "-I", INC] + [f"-D{d}" for d in defines] + ["-o", mi_so, mi_src])
         built.append(mi_so)
     if force or _stale(odp_so, [odp_src, mi_so] + hdrs):
         _run(["gcc", "-O2", "-std=c11", "-Wall", "-Wextra", "-fPIC", "-shared", "-I", INC,
-              "-o", odp_so, odp_src, "-L", PKG, "-lmi_cls", "-Wl,-rpath,$ORIGIN", "-lpthread"])
+              "-o", odp_so, odp_src, "-L", out_dir, "-lmi_cls", "-Wl,-rpath,$ORIGIN",
+              "-lpthread"])
         built.append(odp_so)
     return built
 
 
 if __name__ == "__main__":
-    print(build(force=True))
+    import sys
+    if len(sys.argv) > 2:   # python -m odp_amd._build OUT_DIR DEF=1 ...
+        print(build(force=True, out_dir=sys.argv[1], defines=sys.argv[2:]))
+    else:
+        print(build(force=True))

@@ -17,8 +17,10 @@ import numpy as np
 from . import rules as R
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_MI = os.path.join(_HERE, "libmi_cls.so")
-LIB_ODP = os.path.join(_HERE, "libodp_cls.so")
+# ODP_AMD_LIB_DIR selects an alternative build (kernel variants for A/B runs)
+_LIBDIR = os.environ.get("ODP_AMD_LIB_DIR", _HERE)
+LIB_MI = os.path.join(_LIBDIR, "libmi_cls.so")
+LIB_ODP = os.path.join(_LIBDIR, "libodp_cls.so")
 
 
 class PmrParam(C.Structure):

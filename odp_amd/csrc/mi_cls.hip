@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 #include <errno.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -38,10 +39,21 @@
 #include <vector>
 
 #define WAVE 64
+#ifndef WAVES_PER_BLOCK
 #define WAVES_PER_BLOCK 4
+#endif
 #define BLOCK (WAVE * WAVES_PER_BLOCK)
-#define WIN 128            // staged header window, bytes
-#define WSTRIDE 33         // dwords per packet window in LDS (32 + 1 pad)
+#ifndef WIN
+#define WIN 128            // staged header window, bytes (multiple of 16)
+#endif
+#define WROWS (WIN / 4 + 1)     // LDS dword rows per wave window (+1 zero row)
+#define NPIECE (WIN / 16)       // 16-B pieces per window
+#ifndef MIN_WAVES_PER_EU
+#define MIN_WAVES_PER_EU 1
+#endif
+#ifndef PREFETCH
+#define PREFETCH 1          // software-pipeline the next tile's loads
+#endif
 #define MAX_STATS_COS 256
 
 // ---------------------------------------------------------------- flags
@@ -79,8 +91,12 @@
 #define E_SCTP 32u
 
 // ------------------------------------------------------- packet byte access
+// The LDS window of a wave is dword-major, lane-minor: dword i of lane l's
+// packet lives at W[i * WAVE + l].  Any per-lane byte offset then reads
+// conflict-free (lane l always hits bank l mod 32), whatever the packets'
+// header layouts.
 struct Pkt {
-	const uint32_t *w;      // this lane's LDS window (dwords)
+	const uint32_t *w;      // &W[lane]
 	const uint8_t *g;       // packet start in HBM
 	uint32_t len;           // frame_len
 };
@@ -88,7 +104,7 @@ struct Pkt {
 __device__ __forceinline__ uint32_t rb(const Pkt &k, uint32_t o)
 {
 	if (o < WIN)
-		return (k.w[o >> 2] >> ((o & 3u) * 8u)) & 0xffu;
+		return (k.w[(o >> 2) * WAVE] >> ((o & 3u) * 8u)) & 0xffu;
 	return o < k.len ? (uint32_t)k.g[o] : 0u;
 }
 
@@ -97,7 +113,7 @@ __device__ __forceinline__ uint32_t r32(const Pkt &k, uint32_t o)
 {
 	if (o <= WIN - 4u) {
 		uint32_t i = o >> 2;
-		return __builtin_amdgcn_alignbyte(k.w[i + 1], k.w[i], o & 3u);
+		return __builtin_amdgcn_alignbyte(k.w[(i + 1) * WAVE], k.w[i * WAVE], o & 3u);
 	}
 	return rb(k, o) | (rb(k, o + 1) << 8) | (rb(k, o + 2) << 16) | (rb(k, o + 3) << 24);
 }
@@ -303,6 +319,212 @@ __device__ __forceinline__ Parsed parse_packet(const Pkt &k)
 	return r;
 }
 
+// Branch-light parse for the common header shapes.  Under _odp_parse_eth's
+// rules the L3 offset is one of 14/18/22/26/30 (DIX or SNAP, plus 0-2 tags),
+// so l3 and every L4 offset reached from it are 2 (mod 4): the parse becomes
+// three batches of independent LDS reads (bytes 0-31, the IP header, the
+// L4 header) combined with selects instead of a branch chain.  Lanes it does
+// not cover -- IPv6 HBH/routing chains, or a field past the staged window --
+// report `slow` and take parse_packet() instead; for every other lane the
+// result is identical to parse_packet's.
+__device__ __forceinline__ uint32_t bsw16(uint32_t v)   // be16 of the low half
+{
+	return ((v & 0xffu) << 8) | ((v >> 8) & 0xffu);
+}
+
+__device__ __forceinline__ Parsed parse_fast(const Pkt &k, bool &slow)
+{
+	Parsed r;
+	const uint32_t len = k.len;
+	uint32_t w[8];
+#pragma unroll
+	for (int i = 0; i < 8; ++i)
+		w[i] = k.w[i * WAVE];
+
+	uint32_t f = F_L2 | F_ETH;
+	if (len > 1514u)
+		f |= F_JUMBO;
+	if (w[0] & 1u)
+		f |= F_ETH_MCAST;
+	if (w[0] == 0xffffffffu && (w[1] & 0xffffu) == 0xffffu)
+		f |= F_ETH_BCAST;
+	const uint32_t et0 = bsw16(w[3]);
+	const bool snap = et0 < 1514u;
+	const bool snap_err = snap && et0 > len - 14u;
+	uint32_t e = snap ? bsw16(w[5]) : et0;
+	uint32_t off = snap ? 22u : 14u;
+	// outer tag: type at off+2 = 16 / 24
+	const bool qinq = e == 0x88A8u;
+	if (qinq) {
+		e = snap ? bsw16(w[6]) : bsw16(w[4]);
+		off += 4u;
+	}
+	// inner tag: type at off+2 = 16 / 20 / 24 / 28
+	const bool vlan = e == 0x8100u;
+	if (vlan) {
+		const uint32_t j = (off + 2u) >> 2;
+		const uint32_t wv = j == 4u ? w[4] : (j == 5u ? w[5] : (j == 6u ? w[6] : w[7]));
+		e = bsw16(wv);
+		off += 4u;
+	}
+	uint32_t err = 0;
+	if (snap_err) {
+		err = E_SNAP;
+		e = 0;
+		off = 14u;
+	} else {
+		if (qinq)
+			f |= F_QINQ | F_VLAN;
+		if (vlan)
+			f |= F_VLAN;
+		if (off > len) {
+			f = F_L2;
+			e = 0;
+		}
+	}
+	const uint32_t l3 = off;
+	r.l3 = l3;
+
+	// IP header bytes l3 .. l3+27 (dwords jb .. jb+7, byte shift 2)
+	const uint32_t jb = (l3 - 2u) >> 2;
+	uint32_t h[8];
+#pragma unroll
+	for (int i = 0; i < 8; ++i)
+		h[i] = k.w[(jb + i) * WAVE];
+	uint32_t hb[7];
+#pragma unroll
+	for (int i = 0; i < 7; ++i)
+		hb[i] = __builtin_amdgcn_alignbyte(h[i + 1], h[i], 2u);   // bytes l3+4i .. +3
+
+	const bool is4 = e == 0x0800u, is6 = e == 0x86DDu, isarp = e == 0x0806u;
+	uint32_t ip_proto = 255u, l4 = 0xFFFFu;
+	bool non_first = false;
+	slow = false;
+	if (is4 || is6 || isarp)
+		f |= F_L3;
+	if (isarp)
+		f |= F_ARP;
+	if (is4) {
+		f |= F_IPV4;
+		const uint32_t vi = hb[0] & 0xffu, ihl = vi & 0xfu;
+		const uint32_t tot = bsw16(hb[0] >> 16);
+		if (ihl < 5u || (vi >> 4) != 4u || 20u > len - l3 || tot > len - l3) {
+			err |= E_IP;
+			ip_proto = 0;
+		} else {
+			const uint32_t frag = bsw16(hb[1] >> 16);
+			const uint32_t dst = __builtin_bswap32(hb[4]);
+			l4 = l3 + ihl * 4u;
+			if (ihl > 5u)
+				f |= F_IPOPT;
+			if (frag & 0x3fffu)
+				f |= F_IPFRAG;
+			non_first = (frag & 0x1fffu) != 0;
+			if (dst == 0xffffffffu)
+				f |= F_IP_BCAST;
+			if ((dst >> 28) == 0xeu)
+				f |= F_IP_MCAST;
+			ip_proto = (hb[2] >> 8) & 0xffu;
+		}
+	} else if (is6) {
+		f |= F_IPV6;
+		const uint32_t plen = bsw16(hb[1]);
+		if (((hb[0] & 0xffu) >> 4) != 6u || 40u > len - l3 || plen + 40u > len - l3) {
+			err |= E_IP;
+			ip_proto = 0;
+		} else {
+			if ((hb[6] & 0xffu) == 0xffu)
+				f |= F_IP_MCAST;
+			const uint32_t nh = (hb[1] >> 16) & 0xffu;
+			if (nh == 0u || nh == 43u)
+				slow = true;                 // extension chain: general parser
+			if (nh == 44u)
+				f |= F_IPOPT | F_IPFRAG;
+			ip_proto = nh;
+			l4 = l3 + 40u;
+		}
+	}
+
+	const bool l4hdr = (ip_proto == 6u || ip_proto == 17u || ip_proto == 132u) && !non_first;
+	// L4 header bytes l4 .. l4+15 (dwords jl .. jl+4, byte shift 2)
+	uint32_t lb[4] = { 0, 0, 0, 0 };
+	if (l4hdr) {
+		if (l4 + 18u > WIN) {
+			slow = true;                         // past the staged window
+		} else {
+			const uint32_t jl = (l4 - 2u) >> 2;
+			uint32_t m[5];
+#pragma unroll
+			for (int i = 0; i < 5; ++i)
+				m[i] = k.w[(jl + i) * WAVE];
+#pragma unroll
+			for (int i = 0; i < 4; ++i)
+				lb[i] = __builtin_amdgcn_alignbyte(m[i + 1], m[i], 2u);
+		}
+	}
+	int ret = 0;
+	f |= F_L4;
+	switch (ip_proto) {
+	case 1u:
+	case 58u:
+		f |= F_ICMP;
+		break;
+	case 4u:
+		break;
+	case 6u:
+		f |= F_TCP;
+		if (!non_first) {
+			if (l4 + 20u > len)
+				ret = -1;
+			else if (((lb[3] & 0xffu) >> 4) < 5u)
+				err |= E_TCP;
+		}
+		break;
+	case 17u:
+		f |= F_UDP;
+		if (!non_first) {
+			if (l4 + 8u > len) {
+				ret = -1;
+			} else {
+				const uint32_t ulen = bsw16(lb[1]);
+				if (ulen < 8u)
+					err |= E_UDP;
+				else if ((lb[0] >> 16) == 0x9411u && ulen > 4u && lb[2] != 0u)
+					f |= F_IPSEC;
+			}
+		}
+		break;
+	case 51u:
+		f |= F_IPSEC | F_AH;
+		break;
+	case 50u:
+		f |= F_IPSEC | F_ESP;
+		break;
+	case 132u:
+		f |= F_SCTP;
+		if (!non_first) {
+			if (l4 + 12u > len)
+				ret = -1;
+			else if (((len - l4) & 0xffffu) < 12u)
+				err |= E_SCTP;
+		}
+		break;
+	case 59u:
+		f |= F_NO_NEXT;
+		break;
+	default:
+		f &= ~F_L4;
+		break;
+	}
+	if (!is4 && !is6 && !isarp)
+		f &= ~F_L3;
+	r.l4 = l4;
+	r.flags = f;
+	r.err = err;
+	r.ret = ret < 0 ? -1 : (err != 0 ? 1 : 0);
+	return r;
+}
+
 // --------------------------------------------------------- field registers
 // Gate bits (presence tests of the verify_pmr_<term> helpers)
 #define G_ETH   (1u << 0)
@@ -400,7 +622,7 @@ __device__ __forceinline__ uint32_t thash_word(uint32_t w, uint32_t j)
 }
 
 // packet_rss_hash, odp_classification.c:1773-1839
-__device__ uint32_t rss_hash(const Pkt &k, const Parsed &p, uint32_t hp)
+__device__ __forceinline__ uint32_t rss_hash(const Pkt &k, const Parsed &p, uint32_t hp)
 {
 	const uint32_t f = p.flags;
 	uint32_t h = 0, j = 0;
@@ -552,9 +774,12 @@ __device__ __forceinline__ bool term_ok(cword_t prog, uint32_t &q, const Pkt &k,
 		break;
 	case MI_K_SIP6:
 	case MI_K_DIP6: {
-		const uint32_t *a = (kind == MI_K_SIP6) ? x.s6 : x.d6;
-		ok = (g & G_V6) && eq1(a[0], m0, v0) && eq1(a[1], prog[q + 3], prog[q + 4]) &&
-		     eq1(a[2], prog[q + 5], prog[q + 6]) && eq1(a[3], prog[q + 7], prog[q + 8]);
+		// element-wise select: a pointer select would put the arrays on the stack
+		const bool src = kind == MI_K_SIP6;
+		ok = (g & G_V6) && eq1(src ? x.s6[0] : x.d6[0], m0, v0) &&
+		     eq1(src ? x.s6[1] : x.d6[1], prog[q + 3], prog[q + 4]) &&
+		     eq1(src ? x.s6[2] : x.d6[2], prog[q + 5], prog[q + 6]) &&
+		     eq1(src ? x.s6[3] : x.d6[3], prog[q + 7], prog[q + 8]);
 		q += 6;
 		break;
 	}
@@ -635,11 +860,11 @@ __device__ __forceinline__ bool bv_key(cword_t cr, const Pkt &k, const Parsed &p
 		return g & G_V4;
 	case MI_K_SIP6:
 	case MI_K_DIP6: {
-		const uint32_t *a = (kind == MI_K_SIP6) ? x.s6 : x.d6;
-		key[0] = a[0] & m0;
-		key[1] = a[1] & m1;
-		key[2] = a[2] & m2;
-		key[3] = a[3] & m3;
+		const bool src = kind == MI_K_SIP6;
+		key[0] = (src ? x.s6[0] : x.d6[0]) & m0;
+		key[1] = (src ? x.s6[1] : x.d6[1]) & m1;
+		key[2] = (src ? x.s6[2] : x.d6[2]) & m2;
+		key[3] = (src ? x.s6[3] : x.d6[3]) & m3;
 		return g & G_V6;
 	}
 	case MI_K_SPI:
@@ -778,6 +1003,23 @@ __device__ __forceinline__ void linear_scan(cword_t prog, uint32_t rec0, uint32_
 	}
 }
 
+// Diagnostic build only (-DDIAG_STAMPS): per-phase cycle sums per wave,
+// written to a debug buffer nobody else reads (cdna_hip_programming.md §7).
+#ifdef DIAG_STAMPS
+#define NSTAMP 8
+#define STAMP(i)                                                                   \
+	do {                                                                       \
+		__builtin_amdgcn_sched_barrier(0);                                 \
+		unsigned long long t_;                                             \
+		asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_) :: "memory"); \
+		__builtin_amdgcn_sched_barrier(0);                                 \
+		st_acc[i] += t_ - st_last;                                         \
+		st_last = t_;                                                      \
+	} while (0)
+#else
+#define STAMP(i) do { } while (0)
+#endif
+
 // ------------------------------------------------------------------ kernel
 struct KArgs {
 	const uint8_t *pkts;
@@ -787,6 +1029,7 @@ struct KArgs {
 	const uint32_t *dev;         // device rule program (constant address space)
 	mi_cls_result_t *out;
 	unsigned long long *stats;   // MAX_STATS_COS counters, or NULL
+	unsigned long long *diag;    // DIAG_STAMPS builds only
 	uint32_t stats_mask[8];
 };
 
@@ -806,14 +1049,14 @@ __device__ __forceinline__ void wave_lds_sync()
 	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__global__ __launch_bounds__(BLOCK) void mi_cls_kernel(KArgs a)
+__global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_EU) void mi_cls_kernel(KArgs a)
 {
-	__shared__ uint32_t s_win[WAVES_PER_BLOCK * WAVE * WSTRIDE];
+	__shared__ uint32_t s_win[WAVES_PER_BLOCK * WAVE * WROWS];
 	__shared__ uint32_t s_cnt[MAX_STATS_COS];
 
 	const uint32_t lane = threadIdx.x & (WAVE - 1);
 	const uint32_t wave = threadIdx.x >> 6;
-	uint32_t *W = s_win + wave * WAVE * WSTRIDE;
+	uint32_t *W = s_win + wave * WAVE * WROWS;
 
 	const cword_t dev = (cword_t)a.dev;
 	const int32_t def_cos = (int32_t)dev[DH_DEFAULT];
@@ -831,67 +1074,123 @@ __global__ __launch_bounds__(BLOCK) void mi_cls_kernel(KArgs a)
 		__syncthreads();
 	}
 
+	// Software pipeline over this wave's tiles (64 packets each): while tile
+	// t is parsed and classified, tile t+1's header windows are in flight
+	// into registers and tile t+2's descriptors are being fetched.  Each
+	// lane loads its own packet's window (NPIECE x 16 B).
 	const uint32_t nt = (a.n + WAVE - 1) / WAVE;
-	for (uint32_t tile = blockIdx.x * WAVES_PER_BLOCK + wave; tile < nt;
-	     tile += gridDim.x * WAVES_PER_BLOCK) {
+	const uint32_t tstride = gridDim.x * WAVES_PER_BLOCK;
+	uint32_t tile = blockIdx.x * WAVES_PER_BLOCK + wave;
+	uint32_t d_off = 0, d_len = 0, n_off = 0, n_len = 0;
+	uint4 d[NPIECE];
+	{
+		const uint32_t p0 = tile * WAVE + lane, p1 = (tile + tstride) * WAVE + lane;
+		if (tile < nt && p0 < a.n) {
+			d_off = a.off[p0];
+			d_len = a.len[p0];
+		}
+		if (tile + tstride < nt && p1 < a.n) {
+			n_off = a.off[p1];
+			n_len = a.len[p1];
+		}
+#pragma unroll
+		for (uint32_t r = 0; r < NPIECE; ++r) {
+			d[r] = make_uint4(0, 0, 0, 0);
+#ifndef DIAG_NOLOAD
+			if (16u * r < d_len)
+				__builtin_memcpy(&d[r], a.pkts + d_off + 16u * r, 16);
+#endif
+		}
+	}
+#ifdef DIAG_STAMPS
+	unsigned long long st_acc[NSTAMP] = { 0 }, st_last;
+	asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_last) :: "memory");
+#endif
+	for (; tile < nt; tile += tstride) {
 		const uint32_t pi = tile * WAVE + lane;
 		const bool valid = pi < a.n;
-		const uint32_t my_off = valid ? a.off[pi] : 0u;
-		const uint32_t my_len = valid ? (uint32_t)a.len[pi] : 0u;
+		if (!PREFETCH && tile != blockIdx.x * WAVES_PER_BLOCK + wave) {
+			d_off = valid ? a.off[pi] : 0u;
+			d_len = valid ? (uint32_t)a.len[pi] : 0u;
+#pragma unroll
+			for (uint32_t r = 0; r < NPIECE; ++r) {
+				d[r] = make_uint4(0, 0, 0, 0);
+				if (16u * r < d_len)
+					__builtin_memcpy(&d[r], a.pkts + d_off + 16u * r, 16);
+			}
+		}
+		const uint32_t my_off = d_off, my_len = d_len;
 
-		// ---- stage the first WIN bytes of the wave's 64 packets into LDS.
-		// Phase 1 issues every 16-B load before any is consumed (one HBM
-		// round trip per tile, not eight).
-		uint32_t q_off[8], q_len[8];
-		uint4 d[8];
-#pragma unroll
-		for (uint32_t r = 0; r < 8; ++r) {
-			const uint32_t q = r * 8u + (lane >> 3);
-			q_off[r] = __shfl(my_off, (int)q);
-			q_len[r] = __shfl(my_len, (int)q);
-		}
-#pragma unroll
-		for (uint32_t r = 0; r < 8; ++r) {
-			const uint32_t b0 = (lane & 7u) * 16u;
-			d[r] = make_uint4(0, 0, 0, 0);
-			// gfx950 global loads tolerate any alignment; 16-B aligned frames
-			// (the batch layout's contract) take the full-rate path
-			if (b0 < q_len[r])
-				__builtin_memcpy(&d[r], a.pkts + q_off[r] + b0, 16);
-		}
 		wave_lds_sync();   // previous tile's window reads are done
 #pragma unroll
-		for (uint32_t r = 0; r < 8; ++r) {
-			const uint32_t q = r * 8u + (lane >> 3);
-			const uint32_t b0 = (lane & 7u) * 16u;
+		for (uint32_t r = 0; r < NPIECE; ++r) {
 			uint32_t t[4] = { d[r].x, d[r].y, d[r].z, d[r].w };
-			if (b0 < q_len[r]) {
-				const uint32_t rem = q_len[r] - b0;   // frame bytes in this piece
-				if (rem < 16u) {
+			const uint32_t b0 = 16u * r;
+			// zero the bytes past the frame (reads beyond frame_len give 0)
+			// only the piece holding the frame's last byte is partial; pieces
+			// past the frame were never loaded and are already zero
+			const uint32_t rem = my_len - b0;
+			if (my_len > b0 && rem < 16u) {
 #pragma unroll
-					for (uint32_t i = 0; i < 4; ++i) {
-						const uint32_t lo = 4u * i;
-						const uint32_t keep = rem <= lo ? 0u : (rem >= lo + 4u ? 0xffffffffu
-							: (0xffffffffu >> (8u * (lo + 4u - rem))));
-						t[i] &= keep;
-					}
+				for (uint32_t i = 0; i < 4; ++i) {
+					const uint32_t lo = 4u * i;
+					const uint32_t keep = rem <= lo ? 0u : (rem >= lo + 4u ? 0xffffffffu
+						: (0xffffffffu >> (8u * (lo + 4u - rem))));
+					t[i] &= keep;
 				}
 			}
-			uint32_t *dst = W + q * WSTRIDE + (lane & 7u) * 4u;
-			dst[0] = t[0];
-			dst[1] = t[1];
-			dst[2] = t[2];
-			dst[3] = t[3];
+#pragma unroll
+			for (uint32_t i = 0; i < 4; ++i)
+				W[(4u * r + i) * WAVE + lane] = t[i];
 		}
-		W[lane * WSTRIDE + 32] = 0u;
+		W[(WIN / 4) * WAVE + lane] = 0u;
+
+		STAMP(0);   // data of this tile landed in LDS
+		// advance the pipeline: data of tile+stride, descriptors of tile+2*stride
+		if (PREFETCH) {
+			d_off = n_off;
+			d_len = n_len;
+			const uint32_t t2 = tile + 2u * tstride, p2 = t2 * WAVE + lane;
+			n_off = 0;
+			n_len = 0;
+			if (t2 < nt && p2 < a.n) {
+				n_off = a.off[p2];
+				n_len = a.len[p2];
+			}
+#pragma unroll
+			for (uint32_t r = 0; r < NPIECE; ++r) {
+				d[r] = make_uint4(0, 0, 0, 0);
+#ifndef DIAG_NOLOAD
+				if (16u * r < d_len)
+					__builtin_memcpy(&d[r], a.pkts + d_off + 16u * r, 16);
+#endif
+			}
+		}
 		wave_lds_sync();
+#ifdef DIAG_STAGEONLY
+		if (valid) {
+			uint4 rec;
+			rec.x = W[3 * WAVE + lane] ^ W[8 * WAVE + lane];
+			rec.y = my_len;
+			rec.z = 0;
+			rec.w = 0;
+			*(uint4 *)(a.out + pi) = rec;
+		}
+		continue;
+#endif
 
 		Pkt k;
-		k.w = W + lane * WSTRIDE;
+		k.w = W + lane;
 		k.g = a.pkts + my_off;
 		k.len = my_len;
 
-		Parsed p = parse_packet(k);
+		STAMP(1);   // next tile's loads issued
+		bool slow;
+		Parsed p = parse_fast(k, slow);
+		if (__ballot(slow) != 0ull) {
+			if (slow)
+				p = parse_packet(k);
+		}
 
 		// ---- select the starting CoS (cls_select_cos, odp_classification.c:1694-1726)
 		int32_t cur = -1;
@@ -912,6 +1211,7 @@ __global__ __launch_bounds__(BLOCK) void mi_cls_kernel(KArgs a)
 		if (__ballot(pend))
 			load_fields(k, p, used, x);
 
+		STAMP(2);   // parsed, start CoS selected, fields loaded
 		// ---- CoS descent (match_pmr_cos, :1624-1667).  Each round moves every
 		// pending lane one hop: lanes on a bit-vector CoS evaluate it in
 		// parallel (uniformly when they all sit on one CoS -- scalar loads --
@@ -985,6 +1285,7 @@ __global__ __launch_bounds__(BLOCK) void mi_cls_kernel(KArgs a)
 			}
 		}
 
+		STAMP(3);   // descent done
 		// ---- final CoS -> outcome / queue (_odp_cls_classify_packet, :1742-1771)
 		uint32_t flags = p.flags, out_mark = 0, queue = 0, cos_idx = 0xFFu;
 		if (matched && !loop) {
@@ -1037,7 +1338,15 @@ __global__ __launch_bounds__(BLOCK) void mi_cls_kernel(KArgs a)
 			rec.w = (p.l3 & 0xffffu) | ((p.l4 & 0xffffu) << 16);
 			*(uint4 *)(a.out + pi) = rec;
 		}
+		STAMP(4);   // outcome computed, record stored
 	}
+#ifdef DIAG_STAMPS
+	if (lane == 0 && a.diag) {
+		for (int i = 0; i < NSTAMP; ++i)
+			atomicAdd(a.diag + i, st_acc[i]);
+		atomicAdd(a.diag + NSTAMP, 1ull);
+	}
+#endif
 
 	if (stats_on) {
 		__syncthreads();
@@ -1475,13 +1784,42 @@ extern "C" int mi_cls_classify(mi_cls_ctx_t *c, const uint8_t *pkts, const uint3
 	a.dev = c->d_dev;
 	a.out = out;
 	a.stats = c->stats_on ? c->d_stats : nullptr;
+	a.diag = nullptr;
+#ifdef DIAG_STAMPS
+	static unsigned long long *d_diag = nullptr;
+	if (!d_diag)
+		(void)hipMalloc((void **)&d_diag, 16 * sizeof(unsigned long long));
+	(void)hipMemset(d_diag, 0, 16 * sizeof(unsigned long long));
+	a.diag = d_diag;
+#endif
 	memcpy(a.stats_mask, c->stats_mask, sizeof(a.stats_mask));
+	// one wave per 64-packet tile in flight; the grid covers the resident
+	// capacity (blocks per CU) and each wave loops over its tiles with the
+	// load pipeline (MI_CLS_BLOCKS_PER_CU overrides the default of 4)
+	static int per_cu = -1;
+	if (per_cu < 0) {
+		const char *e = getenv("MI_CLS_BLOCKS_PER_CU");
+		per_cu = e ? atoi(e) : 4;
+		if (per_cu < 1)
+			per_cu = 1;
+	}
 	uint32_t tiles = (n + BLOCK - 1) / BLOCK;
-	uint32_t max_grid = (uint32_t)c->num_cu * 8u;
+	uint32_t max_grid = (uint32_t)c->num_cu * (uint32_t)per_cu;
 	uint32_t grid = tiles < max_grid ? tiles : max_grid;
 	hipLaunchKernelGGL(mi_cls_kernel, dim3(grid), dim3(BLOCK), 0, (hipStream_t)stream, a);
 	if (hipGetLastError() != hipSuccess)
 		return -EIO;
+#ifdef DIAG_STAMPS
+	{
+		unsigned long long h[16];
+		(void)hipStreamSynchronize((hipStream_t)stream);
+		(void)hipMemcpy(h, d_diag, sizeof(h), hipMemcpyDeviceToHost);
+		fprintf(stderr, "DIAG waves=%llu cycles/wave:", h[8]);
+		for (int i = 0; i < 5; ++i)
+			fprintf(stderr, " p%d=%.0f", i, (double)h[i] / (double)(h[8] ? h[8] : 1));
+		fprintf(stderr, "\n");
+	}
+#endif
 	return 0;
 }
 
