@@ -34,6 +34,7 @@
 #include "mi_cls.h"
 
 #include <algorithm>
+#include <type_traits>
 #include <array>
 #include <map>
 #include <vector>
@@ -47,9 +48,10 @@
 #define WIN 128            // staged header window, bytes (multiple of 16)
 #endif
 #define WROWS (WIN / 4 + 1)     // LDS dword rows per wave window (+1 zero row)
+#define RS 66                   // LDS row stride of a window, dwords (see load_window)
 #define NPIECE (WIN / 16)       // 16-B pieces per window
 #ifndef MIN_WAVES_PER_EU
-#define MIN_WAVES_PER_EU 1
+#define MIN_WAVES_PER_EU 4
 #endif
 #ifndef PREFETCH
 #define PREFETCH 1          // software-pipeline the next tile's loads
@@ -92,9 +94,9 @@
 
 // ------------------------------------------------------- packet byte access
 // The LDS window of a wave is dword-major, lane-minor: dword i of lane l's
-// packet lives at W[i * WAVE + l].  Any per-lane byte offset then reads
-// conflict-free (lane l always hits bank l mod 32), whatever the packets'
-// header layouts.
+// packet lives at W[i * RS + l] (RS = 66).  Any per-lane byte offset then
+// reads conflict-free (lane l of row i hits bank 2i + l mod 32), whatever the
+// packets' header layouts.
 struct Pkt {
 	const uint32_t *w;      // &W[lane]
 	const uint8_t *g;       // packet start in HBM
@@ -104,7 +106,7 @@ struct Pkt {
 __device__ __forceinline__ uint32_t rb(const Pkt &k, uint32_t o)
 {
 	if (o < WIN)
-		return (k.w[(o >> 2) * WAVE] >> ((o & 3u) * 8u)) & 0xffu;
+		return (k.w[(o >> 2) * RS] >> ((o & 3u) * 8u)) & 0xffu;
 	return o < k.len ? (uint32_t)k.g[o] : 0u;
 }
 
@@ -113,7 +115,7 @@ __device__ __forceinline__ uint32_t r32(const Pkt &k, uint32_t o)
 {
 	if (o <= WIN - 4u) {
 		uint32_t i = o >> 2;
-		return __builtin_amdgcn_alignbyte(k.w[(i + 1) * WAVE], k.w[i * WAVE], o & 3u);
+		return __builtin_amdgcn_alignbyte(k.w[(i + 1) * RS], k.w[i * RS], o & 3u);
 	}
 	return rb(k, o) | (rb(k, o + 1) << 8) | (rb(k, o + 2) << 16) | (rb(k, o + 3) << 24);
 }
@@ -332,22 +334,31 @@ __device__ __forceinline__ uint32_t bsw16(uint32_t v)   // be16 of the low half
 	return ((v & 0xffu) << 8) | ((v >> 8) & 0xffu);
 }
 
+// Branch-free parse of the common frame shapes: DIX or SNAP, 0-2 VLAN tags,
+// IPv4 (any IHL / errors), IPv6 without HBH / routing headers, ARP, every L4.
+// The reference places L3 at 14/18/22/26/30, so every L3 and L4 offset here is
+// 2 (mod 4) and all header words are one alignbyte of two window dwords.
+// Written as selects (no data-dependent branches) so the wave runs it with a
+// full exec mask; lanes it cannot finish (IPv6 extension chain, L4 header
+// past the window) set `slow` and are re-parsed by parse_packet.  Results are
+// identical to parse_packet for every lane that does not set `slow`.
 __device__ __forceinline__ Parsed parse_fast(const Pkt &k, bool &slow)
 {
 	Parsed r;
 	const uint32_t len = k.len;
 	uint32_t w[8];
 #pragma unroll
-	for (int i = 0; i < 8; ++i)
-		w[i] = k.w[i * WAVE];
+	for (int i = 0; i < 8; ++i) {
+		w[i] = k.w[i * RS];
+		// opaque register value: keeps the selects below v_cndmask instead of
+		// letting the compiler fold them into an indexed (scratch) load of w[]
+		asm("" : "+v"(w[i]));
+	}
 
 	uint32_t f = F_L2 | F_ETH;
-	if (len > 1514u)
-		f |= F_JUMBO;
-	if (w[0] & 1u)
-		f |= F_ETH_MCAST;
-	if (w[0] == 0xffffffffu && (w[1] & 0xffffu) == 0xffffu)
-		f |= F_ETH_BCAST;
+	f |= len > 1514u ? F_JUMBO : 0u;
+	f |= (w[0] & 1u) ? F_ETH_MCAST : 0u;
+	f |= (w[0] == 0xffffffffu && (w[1] & 0xffffu) == 0xffffu) ? F_ETH_BCAST : 0u;
 	const uint32_t et0 = bsw16(w[3]);
 	const bool snap = et0 < 1514u;
 	const bool snap_err = snap && et0 > len - 14u;
@@ -355,173 +366,110 @@ __device__ __forceinline__ Parsed parse_fast(const Pkt &k, bool &slow)
 	uint32_t off = snap ? 22u : 14u;
 	// outer tag: type at off+2 = 16 / 24
 	const bool qinq = e == 0x88A8u;
-	if (qinq) {
-		e = snap ? bsw16(w[6]) : bsw16(w[4]);
-		off += 4u;
-	}
-	// inner tag: type at off+2 = 16 / 20 / 24 / 28
+	e = qinq ? bsw16(snap ? w[6] : w[4]) : e;
+	off += qinq ? 4u : 0u;
+	// inner tag: type at off+2 = 16 / 20 / 24 / 28 (off = 14 + 8 snap + 4 qinq);
+	// selected by the two booleans, not by an index (an index would make the
+	// compiler spill w[] to scratch)
 	const bool vlan = e == 0x8100u;
-	if (vlan) {
-		const uint32_t j = (off + 2u) >> 2;
-		const uint32_t wv = j == 4u ? w[4] : (j == 5u ? w[5] : (j == 6u ? w[6] : w[7]));
-		e = bsw16(wv);
-		off += 4u;
-	}
-	uint32_t err = 0;
-	if (snap_err) {
-		err = E_SNAP;
-		e = 0;
-		off = 14u;
-	} else {
-		if (qinq)
-			f |= F_QINQ | F_VLAN;
-		if (vlan)
-			f |= F_VLAN;
-		if (off > len) {
-			f = F_L2;
-			e = 0;
-		}
-	}
+	const uint32_t wv = snap ? (qinq ? w[7] : w[6]) : (qinq ? w[5] : w[4]);
+	e = vlan ? bsw16(wv) : e;
+	off += vlan ? 4u : 0u;
+	uint32_t err = snap_err ? E_SNAP : 0u;
+	e = snap_err ? 0u : e;
+	off = snap_err ? 14u : off;
+	f |= (!snap_err && qinq) ? (F_QINQ | F_VLAN) : 0u;
+	f |= (!snap_err && vlan) ? F_VLAN : 0u;
+	const bool short_l2 = !snap_err && off > len;
+	f = short_l2 ? F_L2 : f;
+	e = short_l2 ? 0u : e;
 	const uint32_t l3 = off;
 	r.l3 = l3;
 
 	// IP header bytes l3 .. l3+27 (dwords jb .. jb+7, byte shift 2)
 	const uint32_t jb = (l3 - 2u) >> 2;
-	uint32_t h[8];
+	uint32_t h[8], hb[7];
 #pragma unroll
 	for (int i = 0; i < 8; ++i)
-		h[i] = k.w[(jb + i) * WAVE];
-	uint32_t hb[7];
+		h[i] = k.w[(jb + i) * RS];
 #pragma unroll
 	for (int i = 0; i < 7; ++i)
 		hb[i] = __builtin_amdgcn_alignbyte(h[i + 1], h[i], 2u);   // bytes l3+4i .. +3
 
 	const bool is4 = e == 0x0800u, is6 = e == 0x86DDu, isarp = e == 0x0806u;
-	uint32_t ip_proto = 255u, l4 = 0xFFFFu;
-	bool non_first = false;
-	slow = false;
-	if (is4 || is6 || isarp)
-		f |= F_L3;
-	if (isarp)
-		f |= F_ARP;
-	if (is4) {
-		f |= F_IPV4;
-		const uint32_t vi = hb[0] & 0xffu, ihl = vi & 0xfu;
-		const uint32_t tot = bsw16(hb[0] >> 16);
-		if (ihl < 5u || (vi >> 4) != 4u || 20u > len - l3 || tot > len - l3) {
-			err |= E_IP;
-			ip_proto = 0;
-		} else {
-			const uint32_t frag = bsw16(hb[1] >> 16);
-			const uint32_t dst = __builtin_bswap32(hb[4]);
-			l4 = l3 + ihl * 4u;
-			if (ihl > 5u)
-				f |= F_IPOPT;
-			if (frag & 0x3fffu)
-				f |= F_IPFRAG;
-			non_first = (frag & 0x1fffu) != 0;
-			if (dst == 0xffffffffu)
-				f |= F_IP_BCAST;
-			if ((dst >> 28) == 0xeu)
-				f |= F_IP_MCAST;
-			ip_proto = (hb[2] >> 8) & 0xffu;
-		}
-	} else if (is6) {
-		f |= F_IPV6;
-		const uint32_t plen = bsw16(hb[1]);
-		if (((hb[0] & 0xffu) >> 4) != 6u || 40u > len - l3 || plen + 40u > len - l3) {
-			err |= E_IP;
-			ip_proto = 0;
-		} else {
-			if ((hb[6] & 0xffu) == 0xffu)
-				f |= F_IP_MCAST;
-			const uint32_t nh = (hb[1] >> 16) & 0xffu;
-			if (nh == 0u || nh == 43u)
-				slow = true;                 // extension chain: general parser
-			if (nh == 44u)
-				f |= F_IPOPT | F_IPFRAG;
-			ip_proto = nh;
-			l4 = l3 + 40u;
-		}
-	}
+	f |= (is4 || is6 || isarp) ? F_L3 : 0u;
+	f |= isarp ? F_ARP : 0u;
+	// IPv4 (parse_ipv4, odp_parse.c:112-167)
+	const uint32_t vi = hb[0] & 0xffu, ihl = vi & 0xfu;
+	const uint32_t tot = bsw16(hb[0] >> 16);
+	const bool bad4 = ihl < 5u || (vi >> 4) != 4u || 20u > len - l3 || tot > len - l3;
+	const uint32_t frag = bsw16(hb[1] >> 16);
+	const uint32_t dst = __builtin_bswap32(hb[4]);
+	uint32_t f4 = F_IPV4;
+	f4 |= ihl > 5u ? F_IPOPT : 0u;
+	f4 |= (frag & 0x3fffu) ? F_IPFRAG : 0u;
+	f4 |= dst == 0xffffffffu ? F_IP_BCAST : 0u;
+	f4 |= (dst >> 28) == 0xeu ? F_IP_MCAST : 0u;
+	const bool ok4 = is4 && !bad4;
+	f |= is4 ? (bad4 ? F_IPV4 : f4) : 0u;
+	// IPv6 (parse_ipv6, :174-246)
+	const uint32_t plen = bsw16(hb[1]);
+	const bool bad6 = ((hb[0] & 0xffu) >> 4) != 6u || 40u > len - l3 || plen + 40u > len - l3;
+	const uint32_t nh = (hb[1] >> 16) & 0xffu;
+	uint32_t f6 = F_IPV6;
+	f6 |= (hb[6] & 0xffu) == 0xffu ? F_IP_MCAST : 0u;
+	f6 |= nh == 44u ? (F_IPOPT | F_IPFRAG) : 0u;
+	const bool ok6 = is6 && !bad6;
+	f |= is6 ? (bad6 ? F_IPV6 : f6) : 0u;
+	err |= ((is4 && bad4) || (is6 && bad6)) ? E_IP : 0u;
+	const uint32_t ip_proto = ok4 ? ((hb[2] >> 8) & 0xffu) : (ok6 ? nh : ((is4 || is6) ? 0u : 255u));
+	const uint32_t l4 = ok4 ? l3 + ihl * 4u : (ok6 ? l3 + 40u : 0xFFFFu);
+	const bool non_first = ok4 && (frag & 0x1fffu) != 0u;
+	bool sl = ok6 && (nh == 0u || nh == 43u);   // extension chain: general parser
 
-	const bool l4hdr = (ip_proto == 6u || ip_proto == 17u || ip_proto == 132u) && !non_first;
 	// L4 header bytes l4 .. l4+15 (dwords jl .. jl+4, byte shift 2)
-	uint32_t lb[4] = { 0, 0, 0, 0 };
-	if (l4hdr) {
-		if (l4 + 18u > WIN) {
-			slow = true;                         // past the staged window
-		} else {
-			const uint32_t jl = (l4 - 2u) >> 2;
-			uint32_t m[5];
+	const uint32_t jl = min((l4 - 2u) >> 2, (uint32_t)(WROWS - 5));
+	uint32_t m[5], lb[4];
 #pragma unroll
-			for (int i = 0; i < 5; ++i)
-				m[i] = k.w[(jl + i) * WAVE];
+	for (int i = 0; i < 5; ++i)
+		m[i] = k.w[(jl + i) * RS];
 #pragma unroll
-			for (int i = 0; i < 4; ++i)
-				lb[i] = __builtin_amdgcn_alignbyte(m[i + 1], m[i], 2u);
-		}
-	}
-	int ret = 0;
-	f |= F_L4;
-	switch (ip_proto) {
-	case 1u:
-	case 58u:
-		f |= F_ICMP;
-		break;
-	case 4u:
-		break;
-	case 6u:
-		f |= F_TCP;
-		if (!non_first) {
-			if (l4 + 20u > len)
-				ret = -1;
-			else if (((lb[3] & 0xffu) >> 4) < 5u)
-				err |= E_TCP;
-		}
-		break;
-	case 17u:
-		f |= F_UDP;
-		if (!non_first) {
-			if (l4 + 8u > len) {
-				ret = -1;
-			} else {
-				const uint32_t ulen = bsw16(lb[1]);
-				if (ulen < 8u)
-					err |= E_UDP;
-				else if ((lb[0] >> 16) == 0x9411u && ulen > 4u && lb[2] != 0u)
-					f |= F_IPSEC;
-			}
-		}
-		break;
-	case 51u:
-		f |= F_IPSEC | F_AH;
-		break;
-	case 50u:
-		f |= F_IPSEC | F_ESP;
-		break;
-	case 132u:
-		f |= F_SCTP;
-		if (!non_first) {
-			if (l4 + 12u > len)
-				ret = -1;
-			else if (((len - l4) & 0xffffu) < 12u)
-				err |= E_SCTP;
-		}
-		break;
-	case 59u:
-		f |= F_NO_NEXT;
-		break;
-	default:
-		f &= ~F_L4;
-		break;
-	}
-	if (!is4 && !is6 && !isarp)
-		f &= ~F_L3;
+	for (int i = 0; i < 4; ++i)
+		lb[i] = __builtin_amdgcn_alignbyte(m[i + 1], m[i], 2u);
+	const bool tcp = ip_proto == 6u, udp = ip_proto == 17u, sctp = ip_proto == 132u;
+	sl = sl || ((tcp || udp || sctp) && !non_first && l4 + 18u > WIN);   // past the window
+
+	// L4 (_odp_packet_parse_common_l3_l4, :395-460)
+	const bool icmp = ip_proto == 1u || ip_proto == 58u;
+	const bool ah = ip_proto == 51u, esp = ip_proto == 50u;
+	const bool known = icmp || tcp || udp || sctp || ah || esp || ip_proto == 4u || ip_proto == 59u;
+	f |= known ? F_L4 : 0u;
+	f |= icmp ? F_ICMP : 0u;
+	f |= tcp ? F_TCP : 0u;
+	f |= udp ? F_UDP : 0u;
+	f |= sctp ? F_SCTP : 0u;
+	f |= ah ? (F_IPSEC | F_AH) : 0u;
+	f |= esp ? (F_IPSEC | F_ESP) : 0u;
+	f |= ip_proto == 59u ? F_NO_NEXT : 0u;
+	const bool first = !non_first;
+	// TCP (parse_tcp, :299-316)
+	const bool tcp_drop = tcp && first && l4 + 20u > len;
+	err |= (tcp && first && !tcp_drop && ((lb[3] & 0xffu) >> 4) < 5u) ? E_TCP : 0u;
+	// UDP (parse_udp, :321-354)
+	const bool udp_drop = udp && first && l4 + 8u > len;
+	const uint32_t ulen = bsw16(lb[1]);
+	const bool udp_ok = udp && first && !udp_drop;
+	err |= (udp_ok && ulen < 8u) ? E_UDP : 0u;
+	f |= (udp_ok && ulen >= 8u && (lb[0] >> 16) == 0x9411u && ulen > 4u && lb[2] != 0u) ? F_IPSEC : 0u;
+	// SCTP (parse_sctp, :362-388)
+	const bool sctp_drop = sctp && first && l4 + 12u > len;
+	err |= (sctp && first && !sctp_drop && ((len - l4) & 0xffffu) < 12u) ? E_SCTP : 0u;
+
+	slow = sl;
 	r.l4 = l4;
 	r.flags = f;
 	r.err = err;
-	r.ret = ret < 0 ? -1 : (err != 0 ? 1 : 0);
+	r.ret = (tcp_drop || udp_drop || sctp_drop) ? -1 : (err != 0u ? 1 : 0);
 	return r;
 }
 
@@ -537,68 +485,73 @@ __device__ __forceinline__ Parsed parse_fast(const Pkt &k, bool &slow)
 #define G_SPI   (1u << 7)   // ah || esp
 #define G_L3OK  (1u << 8)   // l2 && l3 valid
 
+// The fields verify_pmr_<term> compares, read on use from the packet window
+// (LDS; HBM past it) rather than cached in registers: the window stays valid
+// for the whole tile, and caching every kind the program might use would
+// hold ~20 VGPRs through the descent.  gates = presence bits of the fields.
 struct Fields {
-	uint32_t gates;
-	uint32_t eth0, ethx, vid0, vidx, pcp0, dmac0, dmac1;
-	uint32_t proto, dscp, ports, sip, dip, spi;
-	uint32_t s6[4], d6[4];
+	Pkt k;
+	uint32_t l3, l4, f, gates;
+	__device__ __forceinline__ uint32_t eth0() const { return r16(k, 12); }
+	__device__ __forceinline__ uint32_t ethx() const { return r16(k, (f & F_QINQ) ? 20u : 16u); }
+	__device__ __forceinline__ uint32_t vid0() const { return r16(k, 14) & 0xff0fu; }
+	__device__ __forceinline__ uint32_t pcp0() const { return (r16(k, 14) & 0xffu) >> 5; }
+	__device__ __forceinline__ uint32_t vidx() const
+	{
+		return r16(k, (f & F_QINQ) ? 18u : 14u) & 0xff0fu;
+	}
+	__device__ __forceinline__ uint32_t dmac0() const { return r32(k, 0); }
+	__device__ __forceinline__ uint32_t dmac1() const { return r16(k, 4); }
+	__device__ __forceinline__ uint32_t proto() const
+	{
+		return (f & F_IPV4) ? rb(k, l3 + 9) : rb(k, l3 + 6);
+	}
+	__device__ __forceinline__ uint32_t dscp() const
+	{
+		return (f & F_IPV4) ? (rb(k, l3 + 1) >> 2) : ((be32(k, l3) & 0x0fc00000u) >> 22);
+	}
+	__device__ __forceinline__ uint32_t ports() const
+	{
+		return (f & (F_UDP | F_TCP)) ? r32(k, l4) : 0u;
+	}
+	__device__ __forceinline__ uint32_t sip() const { return r32(k, l3 + 12); }
+	__device__ __forceinline__ uint32_t dip() const { return r32(k, l3 + 16); }
+	// word i of the IPv6 source (src) or destination address
+	__device__ __forceinline__ uint32_t a6(bool src, uint32_t i) const
+	{
+		return r32(k, l3 + (src ? 8u : 24u) + 4u * i);
+	}
+	__device__ __forceinline__ uint32_t spi() const
+	{
+		return (f & F_AH) ? r32(k, l4 + 4) : r32(k, l4);
+	}
 };
 
-__device__ __forceinline__ void load_fields(const Pkt &k, const Parsed &p, uint32_t used, Fields &x)
+__device__ __forceinline__ uint32_t gates_of(const Parsed &p)
 {
 	const uint32_t f = p.flags;
 	uint32_t g = 0;
-	if (f & F_ETH) g |= G_ETH;
-	if ((f & F_ETH) && (f & F_VLAN)) g |= G_VLAN0;
-	if (f & (F_VLAN | F_QINQ)) g |= G_VLANX;
-	if (f & F_IPV4) g |= G_V4;
-	if (f & F_IPV6) g |= G_V6;
-	if (f & F_UDP) g |= G_UDP;
-	if (f & F_TCP) g |= G_TCP;
-	if (f & (F_AH | F_ESP)) g |= G_SPI;
-	if ((f & F_L2) && p.l3 != 0xFFFFu) g |= G_L3OK;
-	x.gates = g;
-	const bool qinq = (f & F_QINQ) != 0;
-	const uint32_t l3 = p.l3, l4 = p.l4;
-	if (used & (1u << MI_K_ETH0)) x.eth0 = r16(k, 12);
-	if (used & (1u << MI_K_ETHX)) x.ethx = r16(k, qinq ? 20u : 16u);
-	if (used & ((1u << MI_K_VID0) | (1u << MI_K_PCP0))) {
-		uint32_t t = r16(k, 14);
-		x.vid0 = t & 0xff0fu;
-		x.pcp0 = (t & 0xffu) >> 5;
-	}
-	if (used & (1u << MI_K_VIDX)) x.vidx = r16(k, qinq ? 18u : 14u) & 0xff0fu;
-	if (used & (1u << MI_K_DMAC)) {
-		x.dmac0 = r32(k, 0);
-		x.dmac1 = r16(k, 4);
-	}
-	if (used & (1u << MI_K_PROTO))
-		x.proto = (f & F_IPV4) ? rb(k, l3 + 9) : rb(k, l3 + 6);
-	if (used & (1u << MI_K_DSCP)) {
-		if (f & F_IPV4) {
-			x.dscp = rb(k, l3 + 1) >> 2;
-		} else {
-			uint32_t v = be32(k, l3);
-			x.dscp = (v & 0x0fc00000u) >> 22;
-		}
-	}
-	if (used & ((1u << MI_K_UDP_DPORT) | (1u << MI_K_TCP_DPORT) |
-		    (1u << MI_K_UDP_SPORT) | (1u << MI_K_TCP_SPORT)))
-		x.ports = (f & (F_UDP | F_TCP)) ? r32(k, l4) : 0u;
-	if (used & (1u << MI_K_SIP)) x.sip = r32(k, l3 + 12);
-	if (used & (1u << MI_K_DIP)) x.dip = r32(k, l3 + 16);
-	if (used & (1u << MI_K_SIP6)) {
-#pragma unroll
-		for (int i = 0; i < 4; ++i)
-			x.s6[i] = r32(k, l3 + 8 + 4 * i);
-	}
-	if (used & (1u << MI_K_DIP6)) {
-#pragma unroll
-		for (int i = 0; i < 4; ++i)
-			x.d6[i] = r32(k, l3 + 24 + 4 * i);
-	}
-	if (used & (1u << MI_K_SPI))
-		x.spi = (f & F_AH) ? r32(k, l4 + 4) : r32(k, l4);
+	g |= (f & F_ETH) ? G_ETH : 0u;
+	g |= ((f & F_ETH) && (f & F_VLAN)) ? G_VLAN0 : 0u;
+	g |= (f & (F_VLAN | F_QINQ)) ? G_VLANX : 0u;
+	g |= (f & F_IPV4) ? G_V4 : 0u;
+	g |= (f & F_IPV6) ? G_V6 : 0u;
+	g |= (f & F_UDP) ? G_UDP : 0u;
+	g |= (f & F_TCP) ? G_TCP : 0u;
+	g |= (f & (F_AH | F_ESP)) ? G_SPI : 0u;
+	g |= ((f & F_L2) && p.l3 != 0xFFFFu) ? G_L3OK : 0u;
+	return g;
+}
+
+__device__ __forceinline__ Fields fields_of(const Pkt &k, const Parsed &p)
+{
+	Fields x;
+	x.k = k;
+	x.l3 = p.l3;
+	x.l4 = p.l4;
+	x.f = p.flags;
+	x.gates = gates_of(p);
+	return x;
 }
 
 // ----------------------------------------------------------- Toeplitz hash
@@ -656,43 +609,60 @@ __device__ __forceinline__ uint32_t rss_hash(const Pkt &k, const Parsed &p, uint
 
 // ------------------------------------------------------ device rule program
 // mi_cls_rules_load() assembles the mi_cls.h table into this private,
-// read-only encoding, read by the kernel through the constant address space
-// (scalar loads: every lane of a wave tests the same rule):
+// read-only encoding (32-bit words):
 //
-//   words [0, 16)          header  (DH_* below)
-//   words [cos_off, ...)   8 words per CoS slot: rule record index, #rules,
-//                          meta = action | num_queue<<8 | hash_proto<<16 | index<<24,
-//                          valid, bit-vector block offset (0 = linear scan)
-//   words [prog_off, ...)  16-word rule records, CoS rules contiguous in scan order:
-//        w0  = inline terms | ext terms<<4 | mark<<16
+//   [0, 16)              header (DH_* below)
+//   [hot_off, +hot_words)  HOT region -- everything a lane may look up with its
+//                        own (per-lane) index.  All offsets inside it are
+//                        relative to hot_off, so the kernel can read it from
+//                        HBM or from a copy in LDS with the same indices:
+//      CoS table        4 words per CoS slot: #rules, bit-vector block (0 =
+//                       linear scan), meta = action | num_queue<<8 |
+//                       hash_proto<<16 | index<<24, first rule record
+//      BV blocks        see below
+//   [prog_off, ...)      COLD region -- 16-word rule records, read only with
+//                        wave-uniform (scalar) loads by the linear engine:
+//        w0  = inline terms | ext terms<<8 | mark<<16
 //        w1  = dst CoS | ext word offset<<8
 //        w2.. terms: op word (kind | size<<8 | nw<<16), [offset word for custom
 //             kinds], then nw (mask, value) word pairs; terms that do not fit
 //             the 14 inline words continue at the ext offset.
-typedef const __attribute__((address_space(4))) uint32_t *cword_t;
+typedef const __attribute__((address_space(4))) uint32_t *cword_t;   // scalar loads
+typedef const __attribute__((address_space(3))) uint32_t *lword_t;   // LDS
+typedef const __attribute__((address_space(1))) uint32_t *gword_t;   // HBM
 
 enum { DH_MAGIC = 0, DH_NCOS, DH_DEFAULT, DH_ERROR, DH_DEFAULT_VALID, DH_USED, DH_MAX_HOPS,
-       DH_COS_OFF, DH_PROG_OFF, DH_TOTAL, DH_WORDS = 16 };
-#define DEV_MAGIC 0x32564544u   // "DEV2"
+       DH_HOT_OFF, DH_PROG_OFF, DH_TOTAL, DH_HOT_WORDS, DH_WORDS = 16 };
+#define DEV_MAGIC 0x33564544u   // "DEV3"
 #define REC_WORDS 16u
-#define COS_WORDS 8u
+#define COS_WORDS 4u
+#define C_NR 0u
+#define C_BV 1u
+#define C_META 2u
+#define C_REC0 3u
 #define BV_MAX_CLS 8u
 #define BV_CLS_WORDS 16u
 #define BV_EMPTY 0xFFFFFFFFu
+#define BV_NONE 0xFFFFFFFEu
 
 // Bit-vector (BV) block of a CoS, used when its rules fall into at most
 // BV_MAX_CLS key classes.  A key class is one (term kind, mask[, offset,
 // size]) combination; for every class the block holds a hash table
 // key -> bitmap row over the CoS's rules (bit r = rule r's terms of that
 // class all equal the key, or rule r has no term of that class), row 0 being
-// the "no term of this class" row used when the packet lacks the field.
-// A packet's matching rules are the AND of its rows; the lowest set bit is
-// the first rule in scan order whose every term matches -- exactly the rule
-// match_pmr_cos picks (odp_classification.c:1631-1650).
-//   bv[0] = W (32-bit words per row), bv[1] = #classes, bv[2] = alive row offset
-//   bv[4 + 16 k ...] class k: kind, nkey, 0, offset, size, mask[4],
-//                    table mask, table offset, rows offset
-//   table slot: nkey key words + row index (BV_EMPTY = free slot)
+// the "no term of this class" row used when the packet lacks the field or
+// its key is in no rule.  A packet's matching rules are the AND of its rows;
+// the lowest set bit is the first rule in scan order whose every term
+// matches -- exactly the rule match_pmr_cos picks
+// (odp_classification.c:1631-1650).  With a single class the AND is a no-op,
+// so the block is DIRECT: a table slot holds the first live rule of its row
+// and class word 2 the first live rule of row 0 (BV_NONE = no rule).
+//   bv[0] = W (32-bit words per row, 0 when direct), bv[1] = #classes,
+//   bv[2] = alive row, bv[3] = result words (dst | leaf<<8 | mark<<16, one per
+//   rule; leaf = the destination CoS has no rules, so the descent ends there)
+//   bv[4 + 16 k ...] class k: kind, nkey, row-0 first rule (direct), offset,
+//                    size, mask[4], table mask, table offset, rows offset
+//   table slot: nkey key words + row index / first rule (BV_EMPTY = free)
 
 __device__ __forceinline__ bool eq1(uint32_t x, uint32_t m, uint32_t v)
 {
@@ -734,57 +704,57 @@ __device__ __forceinline__ bool term_ok(cword_t prog, uint32_t &q, const Pkt &k,
 		ok = eq1(k.len, m0, v0);
 		break;
 	case MI_K_ETH0:
-		ok = (g & G_ETH) && eq1(x.eth0, m0, v0);
+		ok = (g & G_ETH) && eq1(x.eth0(), m0, v0);
 		break;
 	case MI_K_ETHX:
-		ok = (g & G_VLANX) && eq1(x.ethx, m0, v0);
+		ok = (g & G_VLANX) && eq1(x.ethx(), m0, v0);
 		break;
 	case MI_K_VID0:
-		ok = (g & G_VLAN0) && eq1(x.vid0, m0, v0);
+		ok = (g & G_VLAN0) && eq1(x.vid0(), m0, v0);
 		break;
 	case MI_K_VIDX:
-		ok = (g & G_VLANX) && eq1(x.vidx, m0, v0);
+		ok = (g & G_VLANX) && eq1(x.vidx(), m0, v0);
 		break;
 	case MI_K_PCP0:
-		ok = (g & G_VLAN0) && eq1(x.pcp0, m0, v0);
+		ok = (g & G_VLAN0) && eq1(x.pcp0(), m0, v0);
 		break;
 	case MI_K_DMAC:
-		ok = (g & G_ETH) && eq1(x.dmac0, m0, v0) && eq1(x.dmac1, prog[q + 3], prog[q + 4]);
+		ok = (g & G_ETH) && eq1(x.dmac0(), m0, v0) && eq1(x.dmac1(), prog[q + 3], prog[q + 4]);
 		q += 2;
 		break;
 	case MI_K_PROTO:
-		ok = (g & (G_V4 | G_V6)) && eq1(x.proto, m0, v0);
+		ok = (g & (G_V4 | G_V6)) && eq1(x.proto(), m0, v0);
 		break;
 	case MI_K_DSCP:
-		ok = (g & (G_V4 | G_V6)) && eq1(x.dscp, m0, v0);
+		ok = (g & (G_V4 | G_V6)) && eq1(x.dscp(), m0, v0);
 		break;
 	case MI_K_UDP_DPORT:
 	case MI_K_UDP_SPORT:
-		ok = (g & G_UDP) && eq1(x.ports, m0, v0);
+		ok = (g & G_UDP) && eq1(x.ports(), m0, v0);
 		break;
 	case MI_K_TCP_DPORT:
 	case MI_K_TCP_SPORT:
-		ok = (g & G_TCP) && eq1(x.ports, m0, v0);
+		ok = (g & G_TCP) && eq1(x.ports(), m0, v0);
 		break;
 	case MI_K_SIP:
-		ok = (g & G_V4) && eq1(x.sip, m0, v0);
+		ok = (g & G_V4) && eq1(x.sip(), m0, v0);
 		break;
 	case MI_K_DIP:
-		ok = (g & G_V4) && eq1(x.dip, m0, v0);
+		ok = (g & G_V4) && eq1(x.dip(), m0, v0);
 		break;
 	case MI_K_SIP6:
 	case MI_K_DIP6: {
 		// element-wise select: a pointer select would put the arrays on the stack
 		const bool src = kind == MI_K_SIP6;
-		ok = (g & G_V6) && eq1(src ? x.s6[0] : x.d6[0], m0, v0) &&
-		     eq1(src ? x.s6[1] : x.d6[1], prog[q + 3], prog[q + 4]) &&
-		     eq1(src ? x.s6[2] : x.d6[2], prog[q + 5], prog[q + 6]) &&
-		     eq1(src ? x.s6[3] : x.d6[3], prog[q + 7], prog[q + 8]);
+		ok = (g & G_V6) && eq1(x.a6(src, 0), m0, v0) &&
+		     eq1(x.a6(src, 1), prog[q + 3], prog[q + 4]) &&
+		     eq1(x.a6(src, 2), prog[q + 5], prog[q + 6]) &&
+		     eq1(x.a6(src, 3), prog[q + 7], prog[q + 8]);
 		q += 6;
 		break;
 	}
 	case MI_K_SPI:
-		ok = (g & G_SPI) && eq1(x.spi, m0, v0);
+		ok = (g & G_SPI) && eq1(x.spi(), m0, v0);
 		break;
 	case MI_K_ALWAYS:
 		ok = true;
@@ -806,13 +776,28 @@ __device__ __forceinline__ uint32_t bv_hash(const uint32_t k[4])
 	return h;
 }
 
+// Word readers of a BV block: wave-uniform blocks are read with scalar loads
+// from HBM (DescU), per-lane blocks from the hot region (LDS or HBM, DescL).
+struct DescU {
+	cword_t p;
+	__device__ __forceinline__ uint32_t operator()(uint32_t i) const { return p[i]; }
+	__device__ __forceinline__ DescU at(uint32_t o) const { return DescU{ p + o }; }
+};
+template <typename T> struct DescL {
+	T p;
+	uint32_t b;
+	__device__ __forceinline__ uint32_t operator()(uint32_t i) const { return p[b + i]; }
+	__device__ __forceinline__ DescL at(uint32_t o) const { return DescL{ p, b + o }; }
+};
+
 // Key of a packet for one BV class: the masked field the class's terms
 // compare, and whether the packet has that field at all (the term's gate).
-__device__ __forceinline__ bool bv_key(cword_t cr, const Pkt &k, const Parsed &p, const Fields &x,
+template <typename D>
+__device__ __forceinline__ bool bv_key(const D &cr, const Pkt &k, const Parsed &p, const Fields &x,
 				       uint32_t key[4])
 {
-	const uint32_t kind = cr[0];
-	const uint32_t m0 = cr[5], m1 = cr[6], m2 = cr[7], m3 = cr[8];
+	const uint32_t kind = cr(0);
+	const uint32_t m0 = cr(5);
 	const uint32_t g = x.gates;
 	key[1] = key[2] = key[3] = 0;
 	switch (kind) {
@@ -820,59 +805,59 @@ __device__ __forceinline__ bool bv_key(cword_t cr, const Pkt &k, const Parsed &p
 		key[0] = k.len & m0;
 		return true;
 	case MI_K_ETH0:
-		key[0] = x.eth0 & m0;
+		key[0] = x.eth0() & m0;
 		return g & G_ETH;
 	case MI_K_ETHX:
-		key[0] = x.ethx & m0;
+		key[0] = x.ethx() & m0;
 		return g & G_VLANX;
 	case MI_K_VID0:
-		key[0] = x.vid0 & m0;
+		key[0] = x.vid0() & m0;
 		return g & G_VLAN0;
 	case MI_K_VIDX:
-		key[0] = x.vidx & m0;
+		key[0] = x.vidx() & m0;
 		return g & G_VLANX;
 	case MI_K_PCP0:
-		key[0] = x.pcp0 & m0;
+		key[0] = x.pcp0() & m0;
 		return g & G_VLAN0;
 	case MI_K_DMAC:
-		key[0] = x.dmac0 & m0;
-		key[1] = x.dmac1 & m1;
+		key[0] = x.dmac0() & m0;
+		key[1] = x.dmac1() & cr(6);
 		return g & G_ETH;
 	case MI_K_PROTO:
-		key[0] = x.proto & m0;
+		key[0] = x.proto() & m0;
 		return g & (G_V4 | G_V6);
 	case MI_K_DSCP:
-		key[0] = x.dscp & m0;
+		key[0] = x.dscp() & m0;
 		return g & (G_V4 | G_V6);
 	case MI_K_UDP_DPORT:
 	case MI_K_UDP_SPORT:
-		key[0] = x.ports & m0;
+		key[0] = x.ports() & m0;
 		return g & G_UDP;
 	case MI_K_TCP_DPORT:
 	case MI_K_TCP_SPORT:
-		key[0] = x.ports & m0;
+		key[0] = x.ports() & m0;
 		return g & G_TCP;
 	case MI_K_SIP:
-		key[0] = x.sip & m0;
+		key[0] = x.sip() & m0;
 		return g & G_V4;
 	case MI_K_DIP:
-		key[0] = x.dip & m0;
+		key[0] = x.dip() & m0;
 		return g & G_V4;
 	case MI_K_SIP6:
 	case MI_K_DIP6: {
 		const bool src = kind == MI_K_SIP6;
-		key[0] = (src ? x.s6[0] : x.d6[0]) & m0;
-		key[1] = (src ? x.s6[1] : x.d6[1]) & m1;
-		key[2] = (src ? x.s6[2] : x.d6[2]) & m2;
-		key[3] = (src ? x.s6[3] : x.d6[3]) & m3;
+		key[0] = x.a6(src, 0) & m0;
+		key[1] = x.a6(src, 1) & cr(6);
+		key[2] = x.a6(src, 2) & cr(7);
+		key[3] = x.a6(src, 3) & cr(8);
 		return g & G_V6;
 	}
 	case MI_K_SPI:
-		key[0] = x.spi & m0;
+		key[0] = x.spi() & m0;
 		return g & G_SPI;
 	case MI_K_CUSTOM_FRAME:
 	case MI_K_CUSTOM_L3: {
-		const uint32_t toff = cr[3], sz = cr[4], nk = cr[1];
+		const uint32_t toff = cr(3), sz = cr(4), nk = cr(1);
 		uint32_t o = toff;
 		bool ok = true;
 		if (kind == MI_K_CUSTOM_L3) {
@@ -884,10 +869,10 @@ __device__ __forceinline__ bool bv_key(cword_t cr, const Pkt &k, const Parsed &p
 		if (ok) {
 			key[0] = r32(k, o) & m0;
 			if (nk > 1)
-				key[1] = r32(k, o + 4) & m1;
+				key[1] = r32(k, o + 4) & cr(6);
 			if (nk > 2) {
-				key[2] = r32(k, o + 8) & m2;
-				key[3] = r32(k, o + 12) & m3;
+				key[2] = r32(k, o + 8) & cr(7);
+				key[3] = r32(k, o + 12) & cr(8);
 			}
 		}
 		return ok;
@@ -898,69 +883,86 @@ __device__ __forceinline__ bool bv_key(cword_t cr, const Pkt &k, const Parsed &p
 	}
 }
 
-// Bit-vector evaluation of one CoS for the lanes in `act`.  `blk` is the
-// CoS's BV block and `rec` its first rule record; both may be wave-uniform
-// (scalar loads) or per lane (gathers), decided per call site after inlining.
-// On return, lanes of `act` with a matching rule have done = true and the
-// rule's destination CoS / mark in nxt / nmark.
-__device__ __forceinline__ void bv_eval(cword_t blk, const uint32_t *rec, bool act, const Pkt &k,
-					const Parsed &p, const Fields &x, const uint32_t *dv,
-					bool &done, uint32_t &nxt, uint32_t &nmark)
+// Probe a class's open-addressing table for the lane's key; returns the
+// slot's value (row index / first rule) or `miss` when the key is absent.
+template <typename T>
+__device__ __forceinline__ uint32_t bv_probe(T H, uint32_t tbl, uint32_t tmask, uint32_t nk,
+					     const uint32_t key[4], uint32_t miss)
 {
-	const uint32_t Wd = blk[0], ncls = blk[1], alive = blk[2];
-	uint32_t ridx[BV_MAX_CLS];
+	uint32_t h = bv_hash(key) & tmask;
+	for (uint32_t probe = 0; probe <= tmask; ++probe) {
+		const uint32_t s = tbl + h * (nk + 1u);
+		const uint32_t rw = H[s + nk];
+		if (rw == BV_EMPTY)
+			break;
+		bool eq = H[s] == key[0];
+		if (nk > 1)
+			eq = eq && H[s + 1] == key[1];
+		if (nk > 2)
+			eq = eq && H[s + 2] == key[2] && H[s + 3] == key[3];
+		if (eq)
+			return rw;
+		h = (h + 1u) & tmask;
+	}
+	return miss;
+}
+
+// Bit-vector evaluation of one CoS for the lanes in `act`.  `blk` reads the
+// CoS's BV block (wave-uniform or per lane); H is the hot region the table
+// offsets index.  On return, lanes of `act` with a matching rule have
+// done = true and the rule's destination CoS / mark in nxt / nmark.
+template <typename D, typename T>
+__device__ __forceinline__ void bv_eval(const D &blk, T H, bool act, const Pkt &k, const Parsed &p,
+					const Fields &x, bool &done, uint32_t &nxt, uint32_t &nmark, bool &nleaf)
+{
+	const uint32_t Wd = blk(0), ncls = blk(1), alive = blk(2), res = blk(3);
+	uint32_t first = BV_NONE;
+	if (Wd == 0u) {
+		// direct: one class, the slot holds the first live rule of its row
+		const D cr = blk.at(4u);
+		uint32_t key[4];
+		const bool present = bv_key(cr, k, p, x, key);
+		const uint32_t r0 = cr(2);
+		first = r0;
+		if (act && present)
+			first = bv_probe(H, cr(10), cr(9), cr(1), key, r0);
+	} else {
+		uint32_t ridx[BV_MAX_CLS];
 #pragma unroll
-	for (uint32_t kc = 0; kc < BV_MAX_CLS; ++kc) {
-		ridx[kc] = 0;
-		if (kc < ncls) {
-			const cword_t cr = blk + 4u + BV_CLS_WORDS * kc;
-			const uint32_t nk = cr[1], tmask = cr[9], tbl = cr[10], rows = cr[11];
-			uint32_t key[4];
-			const bool present = bv_key(cr, k, p, x, key);
-			uint32_t row = 0;
-			if (act && present) {
-				uint32_t h = bv_hash(key) & tmask;
-				for (uint32_t probe = 0; probe <= tmask; ++probe) {
-					const uint32_t *sl = dv + tbl + h * (nk + 1u);
-					const uint32_t rw = sl[nk];
-					if (rw == BV_EMPTY)
-						break;
-					bool eq = sl[0] == key[0];
-					if (nk > 1)
-						eq = eq && sl[1] == key[1];
-					if (nk > 2)
-						eq = eq && sl[2] == key[2] && sl[3] == key[3];
-					if (eq) {
-						row = rw;
-						break;
-					}
-					h = (h + 1u) & tmask;
+		for (uint32_t kc = 0; kc < BV_MAX_CLS; ++kc) {
+			ridx[kc] = 0;
+			if (kc < ncls) {
+				const D cr = blk.at(4u + BV_CLS_WORDS * kc);
+				uint32_t key[4];
+				const bool present = bv_key(cr, k, p, x, key);
+				uint32_t row = 0;
+				if (act && present)
+					row = bv_probe(H, cr(10), cr(9), cr(1), key, 0u);
+				ridx[kc] = cr(11) + row * Wd;
+			}
+		}
+		bool found = false;
+		for (uint32_t w = 0; w < Wd; ++w) {
+			if (__ballot(act && !found) == 0ull)
+				break;
+			if (act && !found) {
+				uint32_t acc = H[alive + w];
+#pragma unroll
+				for (uint32_t kc = 0; kc < BV_MAX_CLS; ++kc)
+					if (kc < ncls)
+						acc &= H[ridx[kc] + w];
+				if (acc) {
+					found = true;
+					first = w * 32u + (uint32_t)__builtin_ctz(acc);
 				}
 			}
-			ridx[kc] = rows + row * Wd;
 		}
 	}
-	uint32_t first = 0;
-	bool found = false;
-	for (uint32_t w = 0; w < Wd; ++w) {
-		if (__ballot(act && !found) == 0ull)
-			break;
-		if (act && !found) {
-			uint32_t acc = dv[alive + w];
-#pragma unroll
-			for (uint32_t kc = 0; kc < BV_MAX_CLS; ++kc)
-				if (kc < ncls)
-					acc &= dv[ridx[kc] + w];
-			if (acc) {
-				found = true;
-				first = w * 32u + (uint32_t)__builtin_ctz(acc);
-			}
-		}
-	}
-	if (act && found) {
-		const uint32_t *r = rec + first * REC_WORDS;
-		nxt = r[1] & 0xffu;
-		nmark = r[0] >> 16;
+	if (act && first != BV_NONE) {
+		const uint32_t rw = H[res + first];
+		nxt = rw & 0xffu;
+		nleaf = (rw >> 8) & 1u;
+		nmark = rw >> 16;
 		done = true;
 	}
 }
@@ -1002,7 +1004,6 @@ __device__ __forceinline__ void linear_scan(cword_t prog, uint32_t rec0, uint32_
 		}
 	}
 }
-
 // Diagnostic build only (-DDIAG_STAMPS): per-phase cycle sums per wave,
 // written to a debug buffer nobody else reads (cdna_hip_programming.md §7).
 #ifdef DIAG_STAMPS
@@ -1038,6 +1039,108 @@ __device__ __forceinline__ bool stats_bit(const KArgs &a, uint32_t c)
 	return c < MAX_STATS_COS && ((a.stats_mask[c >> 5] >> (c & 31u)) & 1u);
 }
 
+// Buffer offset no frame byte reaches: num_records of the packet resource, so
+// a load at or past it returns zeros (batches are < 4 GiB: u32 offsets).
+#define OOB_OFF 0xFFFFFE00u
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+static_assert(NPIECE == 8 || NPIECE == 6, "WIN must be 96 or 128");
+#define NB (NPIECE - 4)         // upper pieces (phase B)
+
+// Issue the loads of a tile's header windows (64 packets, per-lane
+// descriptors off/len).  The lanes cooperate so that each load instruction
+// covers whole packets' headers: in phase A lane l loads piece l&3 (bytes
+// 16(l&3) ..) of packet 16r + (l>>2), r = 0..3 -- for back-to-back frames an
+// instruction reads 16 x 64 contiguous bytes instead of 64 scattered pieces,
+// a quarter of the cache-line lookups.  Phase B (pieces 4..) is issued only
+// when some frame of the tile is longer than 64 B (returns true).  Pieces
+// wholly past a frame get an out-of-range offset and read as zero.
+__device__ __forceinline__ bool load_window(__amdgpu_buffer_rsrc_t rs, uint32_t off, uint32_t len,
+					    uint32_t lane, u32x4 d[NPIECE])
+{
+	const uint32_t q = lane & 3u, pp = lane >> 2;
+#pragma unroll
+	for (uint32_t r = 0; r < 4; ++r) {
+		const int src = (int)((16u * r + pp) << 2);
+		const uint32_t o = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)off);
+		const uint32_t L = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)len);
+		const uint32_t vo = 16u * q < L ? o + 16u * q : OOB_OFF;
+		d[r] = __builtin_amdgcn_raw_buffer_load_b128(rs, vo, 0, 0);
+	}
+	const bool hi = __ballot(len > 64u) != 0ull;
+	if (hi) {
+		const uint32_t qb = lane % NB, pb = lane / NB;
+#pragma unroll
+		for (uint32_t r = 0; r < NB; ++r) {
+			const int src = (int)(((64u / NB) * r + pb) << 2);
+			const uint32_t o = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)off);
+			const uint32_t L = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)len);
+			const uint32_t c = 16u * (4u + qb);
+			const uint32_t vo = c < L ? o + c : OOB_OFF;
+			d[4 + r] = __builtin_amdgcn_raw_buffer_load_b128(rs, vo, 0, 0);
+		}
+	}
+	return hi;
+}
+
+// Write a tile's loaded pieces into the transposed window: lane l holds
+// dwords 4q..4q+3 of packet p, which go to rows 4q..4q+3, column p.  With the
+// 66-dword row stride the 64 lanes of one ds_write hit distinct banks
+// (bank = 8q + 2i + p mod 32 within each 32-lane half).  Rows 16.. are
+// rewritten only when this tile has long frames, or zeroed once after a tile
+// that had them (hi_rows tracks whether they hold data).
+__device__ __forceinline__ void store_window(uint32_t *W, uint32_t lane, const u32x4 d[NPIECE],
+					     bool hi, bool &hi_rows)
+{
+	const uint32_t q = lane & 3u, pp = lane >> 2;
+#pragma unroll
+	for (uint32_t r = 0; r < 4; ++r) {
+		const uint32_t base = 4u * q * RS + 16u * r + pp;
+#pragma unroll
+		for (uint32_t i = 0; i < 4; ++i)
+			W[base + i * RS] = d[r][i];
+	}
+	if (hi) {
+		const uint32_t qb = lane % NB, pb = lane / NB;
+#pragma unroll
+		for (uint32_t r = 0; r < NB; ++r) {
+			const uint32_t base = 4u * (4u + qb) * RS + (64u / NB) * r + pb;
+#pragma unroll
+			for (uint32_t i = 0; i < 4; ++i)
+				W[base + i * RS] = d[4 + r][i];
+		}
+	} else if (hi_rows) {
+#pragma unroll
+		for (uint32_t row = 16; row < WIN / 4; ++row)
+			W[row * RS + lane] = 0u;
+	}
+	hi_rows = hi;
+}
+
+// Zero the bytes of the last loaded piece that lie past the frame
+// (frame_len .. end of its 16-B piece): the partial dword byte by byte, then
+// up to three whole dwords.  Writes that are not needed go to the lane's pad
+// dword, which is zero anyway, so every lane issues the same 6 stores.
+__device__ __forceinline__ void zero_tail(uint32_t *W, uint32_t lane, uint32_t len)
+{
+	const uint32_t pad = (WIN / 4) * RS + lane;
+	const uint32_t e = min((len + 15u) & ~15u, (uint32_t)WIN);   // end of loaded bytes
+	const uint32_t dw = len >> 2, b = len & 3u;
+	uint8_t *W8 = (uint8_t *)W;
+#pragma unroll
+	for (uint32_t j = 1; j < 4; ++j) {
+		const bool z = b != 0u && j >= b && len < WIN;
+		const uint32_t at = z ? (dw * RS + lane) * 4u + j : pad * 4u + j;
+		W8[at] = 0;
+	}
+	const uint32_t pd = (len + 3u) >> 2;
+#pragma unroll
+	for (uint32_t i = 0; i < 3; ++i) {
+		const bool z = 4u * (pd + i) < e;
+		W[z ? (pd + i) * RS + lane : pad] = 0u;
+	}
+}
+
 // Make this wave's LDS writes visible to its own later LDS reads by other
 // lanes: LDS ops of one wave complete in order, so a wave-scope fence (which
 // keeps the compiler from reordering) is all that is needed -- no block
@@ -1049,40 +1152,74 @@ __device__ __forceinline__ void wave_lds_sync()
 	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_EU) void mi_cls_kernel(KArgs a)
+// DIV = the program has rules behind rules (a CoS tree), so lanes of a wave
+// can sit on different CoS: such rounds evaluate every lane's own bit-vector
+// block at once instead of one CoS per round.
+// LT = the hot region is copied into LDS at block start (it fits the
+// budget): every per-lane table lookup is then an LDS read and the compute
+// phase issues no vector memory loads, so nothing it waits for sits behind
+// the next tile's prefetch in the (in-order) vmcnt queue.  !LT reads the hot
+// region from HBM (large rule sets).
+extern __shared__ uint32_t s_dyn[];
+
+template <bool LT, bool DIV>
+__global__ __launch_bounds__(BLOCK, DIV ? MIN_WAVES_PER_EU - 1 : MIN_WAVES_PER_EU) void
+mi_cls_kernel(KArgs a)
 {
-	__shared__ uint32_t s_win[WAVES_PER_BLOCK * WAVE * WROWS];
+	__shared__ uint32_t s_win[WAVES_PER_BLOCK * RS * WROWS];
 	__shared__ uint32_t s_cnt[MAX_STATS_COS];
 
 	const uint32_t lane = threadIdx.x & (WAVE - 1);
 	const uint32_t wave = threadIdx.x >> 6;
-	uint32_t *W = s_win + wave * WAVE * WROWS;
+	uint32_t *W = s_win + wave * RS * WROWS;
 
 	const cword_t dev = (cword_t)a.dev;
 	const int32_t def_cos = (int32_t)dev[DH_DEFAULT];
 	const int32_t err_cos = (int32_t)dev[DH_ERROR];
 	const uint32_t def_valid = dev[DH_DEFAULT_VALID];
-	const uint32_t used = dev[DH_USED];
 	const uint32_t max_hops = dev[DH_MAX_HOPS];
-	const cword_t cos_tbl = dev + dev[DH_COS_OFF];
+	const uint32_t hot_off = dev[DH_HOT_OFF];
+	const cword_t hc = dev + hot_off;                 // hot region, scalar reads
 	const cword_t prog = dev + dev[DH_PROG_OFF];
 	const bool stats_on = a.stats != nullptr;
+	typedef typename std::conditional<LT, lword_t, gword_t>::type hot_t;
+	hot_t H;
+	if constexpr (LT) {
+		const uint32_t hw = dev[DH_HOT_WORDS];
+		const gword_t src = (gword_t)(a.dev + hot_off);
+		for (uint32_t i = threadIdx.x; i < hw; i += BLOCK)
+			s_dyn[i] = src[i];
+		H = (lword_t)s_dyn;
+	} else {
+		H = (gword_t)(a.dev + hot_off);
+	}
 
 	if (stats_on) {
 		for (uint32_t i = threadIdx.x; i < MAX_STATS_COS; i += BLOCK)
 			s_cnt[i] = 0;
-		__syncthreads();
 	}
+	if (LT || stats_on)
+		__syncthreads();
 
 	// Software pipeline over this wave's tiles (64 packets each): while tile
 	// t is parsed and classified, tile t+1's header windows are in flight
-	// into registers and tile t+2's descriptors are being fetched.  Each
-	// lane loads its own packet's window (NPIECE x 16 B).
+	// into registers (load_window) and tile t+2's descriptors are being
+	// fetched.  Tile t's result records are stored at the top of iteration
+	// t+1, before tile t+2's loads are issued, so waiting for window data
+	// never waits behind a younger store (vmcnt retires in order), and the
+	// records are not held in registers through parse and classify.
+	const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+		(void *)a.pkts, (short)0, (int)OOB_OFF, 0x00020000);
 	const uint32_t nt = (a.n + WAVE - 1) / WAVE;
 	const uint32_t tstride = gridDim.x * WAVES_PER_BLOCK;
 	uint32_t tile = blockIdx.x * WAVES_PER_BLOCK + wave;
 	uint32_t d_off = 0, d_len = 0, n_off = 0, n_len = 0;
-	uint4 d[NPIECE];
+	u32x4 d[NPIECE];
+	bool d_hi, hi_rows = true;
+	W[(WIN / 4) * RS + lane] = 0u;   // pad row: always zero
+	uint4 prev_rec = make_uint4(0, 0, 0, 0);
+	uint32_t prev_pi = 0;
+	bool prev_valid = false;
 	{
 		const uint32_t p0 = tile * WAVE + lane, p1 = (tile + tstride) * WAVE + lane;
 		if (tile < nt && p0 < a.n) {
@@ -1093,14 +1230,7 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_EU) void mi_cls_kernel(KArgs a
 			n_off = a.off[p1];
 			n_len = a.len[p1];
 		}
-#pragma unroll
-		for (uint32_t r = 0; r < NPIECE; ++r) {
-			d[r] = make_uint4(0, 0, 0, 0);
-#ifndef DIAG_NOLOAD
-			if (16u * r < d_len)
-				__builtin_memcpy(&d[r], a.pkts + d_off + 16u * r, 16);
-#endif
-		}
+		d_hi = load_window(rs, d_off, d_len, lane, d);
 	}
 #ifdef DIAG_STAMPS
 	unsigned long long st_acc[NSTAMP] = { 0 }, st_last;
@@ -1112,38 +1242,18 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_EU) void mi_cls_kernel(KArgs a
 		if (!PREFETCH && tile != blockIdx.x * WAVES_PER_BLOCK + wave) {
 			d_off = valid ? a.off[pi] : 0u;
 			d_len = valid ? (uint32_t)a.len[pi] : 0u;
-#pragma unroll
-			for (uint32_t r = 0; r < NPIECE; ++r) {
-				d[r] = make_uint4(0, 0, 0, 0);
-				if (16u * r < d_len)
-					__builtin_memcpy(&d[r], a.pkts + d_off + 16u * r, 16);
-			}
+			d_hi = load_window(rs, d_off, d_len, lane, d);
 		}
 		const uint32_t my_off = d_off, my_len = d_len;
 
 		wave_lds_sync();   // previous tile's window reads are done
-#pragma unroll
-		for (uint32_t r = 0; r < NPIECE; ++r) {
-			uint32_t t[4] = { d[r].x, d[r].y, d[r].z, d[r].w };
-			const uint32_t b0 = 16u * r;
-			// zero the bytes past the frame (reads beyond frame_len give 0)
-			// only the piece holding the frame's last byte is partial; pieces
-			// past the frame were never loaded and are already zero
-			const uint32_t rem = my_len - b0;
-			if (my_len > b0 && rem < 16u) {
-#pragma unroll
-				for (uint32_t i = 0; i < 4; ++i) {
-					const uint32_t lo = 4u * i;
-					const uint32_t keep = rem <= lo ? 0u : (rem >= lo + 4u ? 0xffffffffu
-						: (0xffffffffu >> (8u * (lo + 4u - rem))));
-					t[i] &= keep;
-				}
-			}
-#pragma unroll
-			for (uint32_t i = 0; i < 4; ++i)
-				W[(4u * r + i) * WAVE + lane] = t[i];
-		}
-		W[(WIN / 4) * WAVE + lane] = 0u;
+		store_window(W, lane, d, d_hi, hi_rows);
+		zero_tail(W, lane, my_len);   // same wave: LDS stores stay in order
+		// previous tile's records: issued before this tile's prefetch, so the
+		// next wait for window data never waits behind a younger store
+		if (prev_valid)
+			*(uint4 *)(a.out + prev_pi) = prev_rec;
+		prev_valid = false;
 
 		STAMP(0);   // data of this tile landed in LDS
 		// advance the pipeline: data of tile+stride, descriptors of tile+2*stride
@@ -1157,20 +1267,13 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_EU) void mi_cls_kernel(KArgs a
 				n_off = a.off[p2];
 				n_len = a.len[p2];
 			}
-#pragma unroll
-			for (uint32_t r = 0; r < NPIECE; ++r) {
-				d[r] = make_uint4(0, 0, 0, 0);
-#ifndef DIAG_NOLOAD
-				if (16u * r < d_len)
-					__builtin_memcpy(&d[r], a.pkts + d_off + 16u * r, 16);
-#endif
-			}
+			d_hi = load_window(rs, d_off, d_len, lane, d);
 		}
 		wave_lds_sync();
 #ifdef DIAG_STAGEONLY
 		if (valid) {
 			uint4 rec;
-			rec.x = W[3 * WAVE + lane] ^ W[8 * WAVE + lane];
+			rec.x = W[3 * RS + lane] ^ W[8 * RS + lane];
 			rec.y = my_len;
 			rec.z = 0;
 			rec.w = 0;
@@ -1191,6 +1294,18 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_EU) void mi_cls_kernel(KArgs a
 			if (slow)
 				p = parse_packet(k);
 		}
+		const Fields x = fields_of(k, p);
+#ifdef DIAG_PARSEONLY
+		if (valid) {
+			uint4 rec;
+			rec.x = p.flags;
+			rec.y = p.err;
+			rec.z = x.gates;
+			rec.w = (p.l3 & 0xffffu) | ((p.l4 & 0xffffu) << 16);
+			*(uint4 *)(a.out + pi) = rec;
+		}
+		continue;
+#endif
 
 		// ---- select the starting CoS (cls_select_cos, odp_classification.c:1694-1726)
 		int32_t cur = -1;
@@ -1207,10 +1322,6 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_EU) void mi_cls_kernel(KArgs a
 			pend = def_cos >= 0 && def_valid;
 		}
 
-		Fields x;
-		if (__ballot(pend))
-			load_fields(k, p, used, x);
-
 		STAMP(2);   // parsed, start CoS selected, fields loaded
 		// ---- CoS descent (match_pmr_cos, :1624-1667).  Each round moves every
 		// pending lane one hop: lanes on a bit-vector CoS evaluate it in
@@ -1223,50 +1334,43 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_EU) void mi_cls_kernel(KArgs a
 			const unsigned long long pm = __ballot(pend);
 			if (pm == 0ull)
 				break;
-			const int32_t c0 = __builtin_amdgcn_readlane(cur, (int)__builtin_ctzll(pm));
-			const bool uniform = __ballot(pend && cur != c0) == 0ull;
-			bool done = false, proc = false;
+			bool done = false, nleaf = false, extra = false;
 			uint32_t nxt = 0, nmark = 0;
-			if (uniform) {
-				const uint32_t rec0 = cos_tbl[COS_WORDS * (uint32_t)c0];
-				const uint32_t nr = cos_tbl[COS_WORDS * (uint32_t)c0 + 1u];
-				const uint32_t bv = cos_tbl[COS_WORDS * (uint32_t)c0 + 4u];
-				proc = pend;
-				if (bv != 0u && nr != 0u)
-					bv_eval(dev + bv, a.dev + dev[DH_PROG_OFF] + rec0 * REC_WORDS, pend, k,
-						p, x, a.dev, done, nxt, nmark);
-				else
-					linear_scan(prog, rec0, nr, pend, k, p, x, done, nxt, nmark);
-			} else {
-				const uint32_t ci = COS_WORDS * (uint32_t)(pend ? cur : c0);
-				const uint32_t my_rec0 = a.dev[dev[DH_COS_OFF] + ci];
-				const uint32_t my_nr = a.dev[dev[DH_COS_OFF] + ci + 1u];
-				const uint32_t my_bv = a.dev[dev[DH_COS_OFF] + ci + 4u];
-				const bool empty = pend && my_nr == 0u;
-				const bool bvl = pend && my_nr != 0u && my_bv != 0u;
-				if (__ballot(bvl))
-					bv_eval((cword_t)(a.dev + my_bv),
-						a.dev + dev[DH_PROG_OFF] + my_rec0 * REC_WORDS, bvl, k, p, x,
-						a.dev, done, nxt, nmark);
-				const bool lin = pend && !empty && !bvl;
-				bool grp = false;
-				const unsigned long long lm = __ballot(lin);
-				if (lm) {
-					const int32_t c1 = __builtin_amdgcn_readlane(cur, (int)__builtin_ctzll(lm));
-					grp = lin && cur == c1;
-					const uint32_t rec1 = cos_tbl[COS_WORDS * (uint32_t)c1];
-					const uint32_t nr1 = cos_tbl[COS_WORDS * (uint32_t)c1 + 1u];
-					bool d1 = false;
-					uint32_t n1 = 0, m1 = 0;
-					linear_scan(prog, rec1, nr1, grp, k, p, x, d1, n1, m1);
-					if (grp) {
-						done = d1;
-						nxt = n1;
-						nmark = m1;
-					}
+			bool act = pend;
+			if constexpr (DIV) {
+				// lanes on different CoS: every lane on a bit-vector CoS
+				// evaluates its own block (gathers from the hot region), lanes
+				// on a CoS without rules finish; the rest go to the uniform
+				// engine below, one CoS per round
+				const int32_t c0 = __builtin_amdgcn_readlane(cur, (int)__builtin_ctzll(pm));
+				if (__ballot(pend && cur != c0) != 0ull) {
+					const uint32_t ci = COS_WORDS * (uint32_t)(pend ? cur : c0);
+					const uint32_t my_nr = H[ci + C_NR];
+					const uint32_t my_bv = H[ci + C_BV];
+					const bool empty = pend && my_nr == 0u;
+					const bool bvl = pend && my_nr != 0u && my_bv != 0u;
+					if (__ballot(bvl))
+						bv_eval(DescL<hot_t>{ H, my_bv }, H, bvl, k, p, x, done, nxt,
+							nmark, nleaf);
+					extra = bvl || empty;
+					act = pend && !extra;
 				}
-				proc = bvl || empty || grp;
 			}
+			// uniform engine: the CoS of the first lane in `act`, evaluated by
+			// every lane sitting on it with the CoS's words in SGPRs
+			bool grp = false;
+			const unsigned long long am = __ballot(act);
+			if (am) {
+				const int32_t c1 = __builtin_amdgcn_readlane(cur, (int)__builtin_ctzll(am));
+				grp = act && cur == c1;
+				const cword_t ce = hc + COS_WORDS * (uint32_t)c1;
+				const uint32_t nr = ce[C_NR], bv = ce[C_BV];
+				if (bv != 0u && nr != 0u)
+					bv_eval(DescU{ hc + bv }, H, grp, k, p, x, done, nxt, nmark, nleaf);
+				else
+					linear_scan(prog, ce[C_REC0], nr, grp, k, p, x, done, nxt, nmark);
+			}
+			const bool proc = extra || grp;
 			if (proc) {
 				if (done) {
 					cur = (int32_t)nxt;
@@ -1278,6 +1382,8 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_EU) void mi_cls_kernel(KArgs a
 					if (hops > max_hops) {
 						loop = true;
 						pend = false;
+					} else if (nleaf) {
+						pend = false;   // no rules at the destination
 					}
 				} else {
 					pend = false;
@@ -1314,7 +1420,7 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_EU) void mi_cls_kernel(KArgs a
 			if (fc < 0) {
 				outcome = MI_CLS_OUT_DISCARD;
 			} else {
-				const uint32_t meta = a.dev[dev[DH_COS_OFF] + COS_WORDS * (uint32_t)fc + 2u];
+				const uint32_t meta = H[COS_WORDS * (uint32_t)fc + C_META];
 				cos_idx = meta >> 24;
 				const uint32_t nq = (meta >> 8) & 0xffu;
 				if (meta & 0xffu) {
@@ -1329,17 +1435,17 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_EU) void mi_cls_kernel(KArgs a
 			}
 		}
 
-		if (valid) {
-			uint4 rec;
-			rec.x = flags;
-			rec.y = (p.err & 0xffu) | ((outcome & 0xffu) << 8) | ((cos_idx & 0xffu) << 16) |
-				((hops & 0xffu) << 24);
-			rec.z = (queue & 0xffffu) | ((out_mark & 0xffffu) << 16);
-			rec.w = (p.l3 & 0xffffu) | ((p.l4 & 0xffffu) << 16);
-			*(uint4 *)(a.out + pi) = rec;
-		}
+		prev_rec.x = flags;
+		prev_rec.y = (p.err & 0xffu) | ((outcome & 0xffu) << 8) | ((cos_idx & 0xffu) << 16) |
+			     ((hops & 0xffu) << 24);
+		prev_rec.z = (queue & 0xffffu) | ((out_mark & 0xffffu) << 16);
+		prev_rec.w = (p.l3 & 0xffffu) | ((p.l4 & 0xffffu) << 16);
+		prev_pi = pi;
+		prev_valid = valid;
 		STAMP(4);   // outcome computed, record stored
 	}
+	if (prev_valid)
+		*(uint4 *)(a.out + prev_pi) = prev_rec;
 #ifdef DIAG_STAMPS
 	if (lane == 0 && a.diag) {
 		for (int i = 0; i < NSTAMP; ++i)
@@ -1362,6 +1468,8 @@ struct mi_cls_ctx {
 	uint32_t *d_dev;         // assembled device rule program
 	size_t dev_cap;          // bytes
 	int loaded;
+	uint32_t hot_words;      // size of the program's hot region
+	int tree;                // some rule leads to a CoS with rules (DIV kernel)
 	unsigned long long *d_stats;
 	int stats_on;
 	uint32_t stats_mask[8];
@@ -1543,8 +1651,8 @@ static bool class_of(const mi_term_t &t, ClassKey &ck)
 // Build the BV block of one CoS into `blk` (word offsets relative to the
 // start of the device program, base = blk's first word index).  Returns false
 // when the CoS needs more than BV_MAX_CLS classes (linear scan instead).
-static bool build_bv(const mi_rule_t *rs, const mi_term_t *ts, uint32_t nrules, uint32_t base,
-		     std::vector<uint32_t> &blk)
+static bool build_bv(const mi_cos_t *cs, const mi_rule_t *rs, const mi_term_t *ts, uint32_t nrules,
+		     uint32_t base, std::vector<uint32_t> &blk)
 {
 	std::map<ClassKey, uint32_t> cls;
 	std::vector<ClassKey> cls_list;
@@ -1600,50 +1708,67 @@ static bool build_bv(const mi_rule_t *rs, const mi_term_t *ts, uint32_t nrules, 
 				dc[c][r >> 5] |= 1u << (r & 31);
 		}
 	}
-	// layout: header (4) | classes (16 each) | alive row | per class: table, rows
+	// layout: header (4) | classes (16 each) | alive row | results |
+	//         per class: table [, rows]
+	const bool direct = ncls == 1;
 	blk.assign(4 + BV_CLS_WORDS * ncls, 0);
-	blk[0] = W;
+	blk[0] = direct ? 0u : W;
 	blk[1] = ncls;
 	blk[2] = base + (uint32_t)blk.size();
 	blk.insert(blk.end(), alive.begin(), alive.end());
+	blk[3] = base + (uint32_t)blk.size();
+	for (uint32_t r = 0; r < nrules; ++r)
+		blk.push_back((rs[r].dst_cos & 0xffu) | (cs[rs[r].dst_cos].num_rules == 0 ? 0x100u : 0u) |
+			      ((uint32_t)rs[r].mark << 16));
+	auto first_live = [&](const std::vector<uint32_t> &bits) -> uint32_t {
+		for (uint32_t i = 0; i < W; ++i)
+			if (bits[i] & alive[i])
+				return i * 32u + (uint32_t)__builtin_ctz(bits[i] & alive[i]);
+		return BV_NONE;
+	};
 	for (uint32_t c = 0; c < ncls; ++c) {
 		const ClassKey &ck = cls_list[c];
 		const uint32_t nvals = (uint32_t)rows_of[c].size();
 		uint32_t tsize = 4;
 		while (tsize < 2 * (nvals + 1))
 			tsize <<= 1;
-		uint32_t *cr = &blk[4 + BV_CLS_WORDS * c];
-		cr[0] = ck.kind;
-		cr[1] = ck.nkey;
-		cr[3] = ck.offset;
-		cr[4] = ck.size;
+		const uint32_t cbase = 4 + BV_CLS_WORDS * c;
+		blk[cbase + 0] = ck.kind;
+		blk[cbase + 1] = ck.nkey;
+		blk[cbase + 2] = direct ? first_live(dc[c]) : 0u;
+		blk[cbase + 3] = ck.offset;
+		blk[cbase + 4] = ck.size;
 		for (int i = 0; i < 4; ++i)
-			cr[5 + i] = ck.mask[i];
-		cr[9] = tsize - 1;
+			blk[cbase + 5 + i] = ck.mask[i];
+		blk[cbase + 9] = tsize - 1;
 		const uint32_t tbl_off = (uint32_t)blk.size();
-		cr = nullptr;
 		blk.resize(blk.size() + (size_t)tsize * (ck.nkey + 1), 0);
 		for (uint32_t i = 0; i < tsize; ++i)
 			blk[tbl_off + i * (ck.nkey + 1) + ck.nkey] = BV_EMPTY;
 		const uint32_t rows_off = (uint32_t)blk.size();
-		// row 0: rules without a term of this class
-		blk.insert(blk.end(), dc[c].begin(), dc[c].end());
+		if (!direct)   // row 0: rules without a term of this class
+			blk.insert(blk.end(), dc[c].begin(), dc[c].end());
 		uint32_t row = 1;
 		for (auto &kv : rows_of[c]) {
 			std::vector<uint32_t> bits = dc[c];
 			for (uint32_t r : kv.second)
 				bits[r >> 5] |= 1u << (r & 31);
-			blk.insert(blk.end(), bits.begin(), bits.end());
+			uint32_t val;
+			if (direct) {
+				val = first_live(bits);
+			} else {
+				blk.insert(blk.end(), bits.begin(), bits.end());
+				val = row++;
+			}
 			uint32_t h = host_bv_hash(kv.first) & (tsize - 1);
 			while (blk[tbl_off + h * (ck.nkey + 1) + ck.nkey] != BV_EMPTY)
 				h = (h + 1) & (tsize - 1);
 			for (uint32_t i = 0; i < ck.nkey; ++i)
 				blk[tbl_off + h * (ck.nkey + 1) + i] = kv.first[i];
-			blk[tbl_off + h * (ck.nkey + 1) + ck.nkey] = row++;
+			blk[tbl_off + h * (ck.nkey + 1) + ck.nkey] = val;
 		}
-		uint32_t *cw = &blk[4 + BV_CLS_WORDS * c];
-		cw[10] = base + tbl_off;
-		cw[11] = base + rows_off;
+		blk[cbase + 10] = base + tbl_off;
+		blk[cbase + 11] = base + rows_off;
 	}
 	return true;
 }
@@ -1656,8 +1781,32 @@ static int assemble(const void *tbl, uint32_t **out, size_t *out_words)
 	const mi_cos_t *cs = (const mi_cos_t *)(b + h->cos_off);
 	const mi_rule_t *rs = (const mi_rule_t *)(b + h->rule_off);
 	const mi_term_t *ts = (const mi_term_t *)(b + h->term_off);
-	const uint32_t cos_off = DH_WORDS, prog_off = cos_off + COS_WORDS * h->num_cos;
+	// hot region: CoS table then the BV blocks (offsets relative to hot_off)
+	std::vector<uint32_t> hot((size_t)COS_WORDS * h->num_cos, 0);
+	for (uint32_t s = 0; s < h->num_cos; ++s) {
+		uint32_t *c = &hot[COS_WORDS * s];
+		c[C_NR] = cs[s].num_rules;
+		c[C_META] = (uint32_t)cs[s].action | ((uint32_t)cs[s].num_queue << 8) |
+			    ((uint32_t)cs[s].hash_proto << 16) | ((uint32_t)cs[s].index << 24);
+		c[C_REC0] = cs[s].rule_begin;
+	}
+	if (!getenv("MI_CLS_NO_BV")) {
+		for (uint32_t s = 0; s < h->num_cos; ++s) {
+			if (!cs[s].valid || cs[s].num_rules == 0)
+				continue;
+			std::vector<uint32_t> blk;
+			const uint32_t base = (uint32_t)hot.size();
+			if (build_bv(cs, rs + cs[s].rule_begin, ts, cs[s].num_rules, base, blk)) {
+				hot[COS_WORDS * s + C_BV] = base;
+				hot.insert(hot.end(), blk.begin(), blk.end());
+			}
+		}
+	}
+	// cold region: 16-word rule records (+ ext terms appended after them)
+	const uint32_t hot_off = DH_WORDS;
+	const size_t prog_off = hot_off + hot.size();
 	std::vector<uint32_t> w(prog_off + (size_t)h->num_rules * REC_WORDS, 0);
+	std::copy(hot.begin(), hot.end(), w.begin() + hot_off);
 	w[DH_MAGIC] = DEV_MAGIC;
 	w[DH_NCOS] = h->num_cos;
 	w[DH_DEFAULT] = (uint32_t)h->default_cos;
@@ -1665,17 +1814,9 @@ static int assemble(const void *tbl, uint32_t **out, size_t *out_words)
 	w[DH_DEFAULT_VALID] = h->default_valid;
 	w[DH_USED] = h->used_kinds;
 	w[DH_MAX_HOPS] = h->max_hops;
-	w[DH_COS_OFF] = cos_off;
-	w[DH_PROG_OFF] = prog_off;
-	for (uint32_t s = 0; s < h->num_cos; ++s) {
-		uint32_t *c = &w[cos_off + COS_WORDS * s];
-		c[0] = cs[s].rule_begin;
-		c[1] = cs[s].num_rules;
-		c[2] = (uint32_t)cs[s].action | ((uint32_t)cs[s].num_queue << 8) |
-		       ((uint32_t)cs[s].hash_proto << 16) | ((uint32_t)cs[s].index << 24);
-		c[3] = cs[s].valid;
-	}
-	// 16-word rule records (+ ext terms appended after them)
+	w[DH_HOT_OFF] = hot_off;
+	w[DH_HOT_WORDS] = (uint32_t)hot.size();
+	w[DH_PROG_OFF] = (uint32_t)prog_off;
 	std::vector<uint32_t> ext;
 	const size_t ext_base = (size_t)h->num_rules * REC_WORDS;
 	for (uint32_t r = 0; r < h->num_rules; ++r) {
@@ -1700,19 +1841,6 @@ static int assemble(const void *tbl, uint32_t **out, size_t *out_words)
 		rec[1] = rs[r].dst_cos | ((uint32_t)(n_ext ? ext_begin : 0) << 8);
 	}
 	w.insert(w.end(), ext.begin(), ext.end());
-	// bit-vector blocks (absolute word offsets)
-	if (!getenv("MI_CLS_NO_BV")) {
-		for (uint32_t s = 0; s < h->num_cos; ++s) {
-			if (!cs[s].valid || cs[s].num_rules == 0)
-				continue;
-			std::vector<uint32_t> blk;
-			const uint32_t base = (uint32_t)w.size();
-			if (build_bv(rs + cs[s].rule_begin, ts, cs[s].num_rules, base, blk)) {
-				w[cos_off + COS_WORDS * s + 4] = base;
-				w.insert(w.end(), blk.begin(), blk.end());
-			}
-		}
-	}
 	w.resize(w.size() + 16, 0);
 	w[DH_TOTAL] = (uint32_t)w.size();
 	uint32_t *o = (uint32_t *)malloc(w.size() * sizeof(uint32_t));
@@ -1736,6 +1864,26 @@ extern "C" int mi_cls_rules_load(mi_cls_ctx_t *c, const void *tbl, size_t bytes,
 	rc = assemble(tbl, &w, &words);
 	if (rc)
 		return rc;
+	const uint32_t hot_words = w[DH_HOT_WORDS];
+	int tree = 0;
+	{
+		// a rule whose destination has rules, or an error CoS with rules
+		// next to a default CoS with rules: lanes of a wave may then sit on
+		// different CoS with rules in one round
+		const mi_tbl_hdr_t *th = (const mi_tbl_hdr_t *)tbl;
+		const mi_cos_t *tc = (const mi_cos_t *)((const uint8_t *)tbl + th->cos_off);
+		const mi_rule_t *tr = (const mi_rule_t *)((const uint8_t *)tbl + th->rule_off);
+		for (uint32_t r = 0; r < th->num_rules && !tree; ++r)
+			tree = tc[tr[r].dst_cos].num_rules != 0;
+		if (th->error_cos >= 0 && th->default_cos >= 0 && tc[th->error_cos].num_rules &&
+		    tc[th->default_cos].num_rules)
+			tree = 1;
+		const char *e = getenv("MI_CLS_DIV");
+		if (e)
+			tree = atoi(e) != 0;
+	}
+	if (getenv("MI_CLS_VERBOSE"))
+		fprintf(stderr, "mi_cls: program %zu words, hot region %u words\n", words, hot_words);
 	size_t nbytes = words * sizeof(uint32_t);
 	if (hipSetDevice(c->device) != hipSuccess)
 		return free(w), -EIO;
@@ -1760,6 +1908,8 @@ extern "C" int mi_cls_rules_load(mi_cls_ctx_t *c, const void *tbl, size_t bytes,
 	free(w);
 	if (e != hipSuccess)
 		return -EIO;
+	c->hot_words = hot_words;
+	c->tree = tree;
 	c->loaded = 1;
 	return 0;
 }
@@ -1793,20 +1943,47 @@ extern "C" int mi_cls_classify(mi_cls_ctx_t *c, const uint8_t *pkts, const uint3
 	a.diag = d_diag;
 #endif
 	memcpy(a.stats_mask, c->stats_mask, sizeof(a.stats_mask));
-	// one wave per 64-packet tile in flight; the grid covers the resident
-	// capacity (blocks per CU) and each wave loops over its tiles with the
-	// load pipeline (MI_CLS_BLOCKS_PER_CU overrides the default of 4)
-	static int per_cu = -1;
-	if (per_cu < 0) {
+	// One wave per 64-packet tile in flight; the grid covers the resident
+	// capacity (blocks per CU: 4 = the VGPR-bound occupancy of 4 waves/SIMD,
+	// fewer when the LDS copy of the hot region does not leave room) and each
+	// wave loops over its tiles with the load pipeline.
+	// MI_CLS_BLOCKS_PER_CU overrides the block count, MI_CLS_LDS_HOT_MAX
+	// (bytes) the largest hot region copied into LDS.
+	static int per_cu_env = -2, hot_max = -1;
+	if (per_cu_env == -2) {
 		const char *e = getenv("MI_CLS_BLOCKS_PER_CU");
-		per_cu = e ? atoi(e) : 4;
-		if (per_cu < 1)
-			per_cu = 1;
+		per_cu_env = e ? atoi(e) : -1;
+		e = getenv("MI_CLS_LDS_HOT_MAX");
+		hot_max = e ? atoi(e) : 20 * 1024;
 	}
+	const size_t hot_bytes = (size_t)c->hot_words * sizeof(uint32_t);
+	const bool lt = (long)hot_bytes <= (long)hot_max;
+	const size_t lds_static = sizeof(uint32_t) * (WAVES_PER_BLOCK * RS * WROWS + MAX_STATS_COS);
+	const size_t lds_block = lds_static + (lt ? hot_bytes : 0);
+	const bool div = c->tree;
+	int per_cu = (int)((160u * 1024u) / lds_block);
+	const int occ = div ? MIN_WAVES_PER_EU - 1 : MIN_WAVES_PER_EU;   // waves/SIMD by VGPRs
+	if (per_cu > occ * 4 / WAVES_PER_BLOCK)
+		per_cu = occ * 4 / WAVES_PER_BLOCK;
+	if (per_cu_env > 0)
+		per_cu = per_cu_env;
+	if (per_cu < 1)
+		per_cu = 1;
 	uint32_t tiles = (n + BLOCK - 1) / BLOCK;
 	uint32_t max_grid = (uint32_t)c->num_cu * (uint32_t)per_cu;
 	uint32_t grid = tiles < max_grid ? tiles : max_grid;
-	hipLaunchKernelGGL(mi_cls_kernel, dim3(grid), dim3(BLOCK), 0, (hipStream_t)stream, a);
+	if (lt && div)
+		hipLaunchKernelGGL((mi_cls_kernel<true, true>), dim3(grid), dim3(BLOCK), hot_bytes,
+				   (hipStream_t)stream, a);
+	else if (lt)
+		hipLaunchKernelGGL((mi_cls_kernel<true, false>), dim3(grid), dim3(BLOCK), hot_bytes,
+				   (hipStream_t)stream, a);
+	else if (div)
+		hipLaunchKernelGGL((mi_cls_kernel<false, true>), dim3(grid), dim3(BLOCK), 0,
+				   (hipStream_t)stream, a);
+	else
+		hipLaunchKernelGGL((mi_cls_kernel<false, false>), dim3(grid), dim3(BLOCK), 0,
+				   (hipStream_t)stream, a);
 	if (hipGetLastError() != hipSuccess)
 		return -EIO;
 #ifdef DIAG_STAMPS

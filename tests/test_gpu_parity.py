@@ -16,19 +16,29 @@ from tests.helpers import assert_same, gpu_run, oracle_run, summary
 pytestmark = pytest.mark.gpu
 
 
+ENGINE_ENV = {
+    "auto": {},
+    "linear": {"MI_CLS_NO_BV": "1"},   # linear scan everywhere
+    "nodiv": {"MI_CLS_DIV": "0"},      # no per-lane bit-vector rounds (CoS waterfall)
+    "div": {"MI_CLS_DIV": "1"},        # per-lane bit-vector rounds even for flat programs
+}
+
+
 def both(prog, batch, limits=(255, 8192, 4096), what="", engine="auto"):
     """engine "auto": bit-vector blocks where a CoS has <= 8 key classes,
-    linear scan otherwise; "linear": force the linear scan everywhere."""
+    linear scan otherwise, per-lane rounds for CoS trees; the other engines
+    force one of the kernel's paths (ENGINE_ENV)."""
     import os
-    old = os.environ.pop("MI_CLS_NO_BV", None)
-    if engine == "linear":
-        os.environ["MI_CLS_NO_BV"] = "1"
+    keys = ("MI_CLS_NO_BV", "MI_CLS_DIV")
+    old = {k: os.environ.pop(k, None) for k in keys}
+    os.environ.update(ENGINE_ENV[engine])
     try:
         got = gpu_run(prog, batch, limits)
     finally:
-        os.environ.pop("MI_CLS_NO_BV", None)
-        if old is not None:
-            os.environ["MI_CLS_NO_BV"] = old
+        for k in keys:
+            os.environ.pop(k, None)
+            if old[k] is not None:
+                os.environ[k] = old[k]
     exp, _ = oracle_run(prog, batch, limits)
     assert_same(got, exp, batch, f"{what} [{engine}]")
     return got
@@ -82,7 +92,7 @@ def test_zoo_no_default(built, gpu):
     assert s["discard"] > 0 and s["cos_drop"] > 0
 
 
-@pytest.mark.parametrize("engine", ["auto", "linear"])
+@pytest.mark.parametrize("engine", ["auto", "linear", "nodiv", "div"])
 @pytest.mark.parametrize("seed", range(12))
 def test_random_programs_fuzz(built, gpu, seed, engine):
     rng = np.random.default_rng(1000 + seed)
@@ -95,7 +105,7 @@ def test_random_programs_fuzz(built, gpu, seed, engine):
     both(prog, b, what=f"fuzz seed {seed}", engine=engine)
 
 
-@pytest.mark.parametrize("engine", ["auto", "linear"])
+@pytest.mark.parametrize("engine", ["auto", "linear", "nodiv"])
 @pytest.mark.parametrize("cfg,n", [(1, 10_000), (2, 100_000), (3, 50_000), (4, 50_000),
                                    (5, 20_000)])
 def test_configs_small(built, gpu, cfg, n, engine):

@@ -1,17 +1,24 @@
 #!/bin/bash
 # A/B kernel variants on the GPU box: build each -D set into its own dir and
-# time the bench's kernel for several workloads.  Usage:
-#   tools/variants.sh "WIN=128" "WIN=64" "WIN=64 MIN_WAVES_PER_EU=2" ...
+# time the bench's kernel for several workloads.  An argument starting with
+# "env " runs the in-tree build with those environment settings instead.
+#   tools/variants.sh "WIN=128" "WIN=64 MIN_WAVES_PER_EU=2" "env MI_CLS_LDS_HOT_MAX=0"
 set -o pipefail
 CFGS=${CFGS:-"20 2 3 5"}
 mkdir -p gpurun_out
 i=0
 for v in "$@"; do
-  d=/tmp/variant_$i
-  timeout -k 10 300 python -m odp_amd._build $d $v > /dev/null || exit 1
+  d=$(pwd)/odp_amd
+  envs=""
+  if [[ "$v" == env\ * ]]; then
+    envs=${v#env }
+  else
+    d=/tmp/variant_$i
+    timeout -k 10 300 python -m odp_amd._build $d $v > /dev/null || exit 1
+  fi
   for c in $CFGS; do
-    ODP_AMD_LIB_DIR=$d timeout -k 10 200 python bench.py --config $c --steps 30 --warmup 5 \
-      --no-cpu --no-extra > /tmp/v.json || exit 1
+    env $envs ODP_AMD_LIB_DIR=$d timeout -k 10 200 python bench.py --config $c --steps 30 --warmup 5 \
+      --no-cpu --no-extra $BENCH_EXTRA > /tmp/v.json || exit 1
     python -c "import json; d=json.load(open('/tmp/v.json')); print('$v', d['config']['workload'], d['config']['rules'], d['roofline']['kernel_ms'], d['value'])"
   done
   i=$((i+1))
