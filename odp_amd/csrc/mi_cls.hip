@@ -485,47 +485,93 @@ __device__ __forceinline__ Parsed parse_fast(const Pkt &k, bool &slow)
 #define G_SPI   (1u << 7)   // ah || esp
 #define G_L3OK  (1u << 8)   // l2 && l3 valid
 
-// The fields verify_pmr_<term> compares, read on use from the packet window
+// What the term verifiers compare is read on use from the packet window
 // (LDS; HBM past it) rather than cached in registers: the window stays valid
 // for the whole tile, and caching every kind the program might use would
 // hold ~20 VGPRs through the descent.  gates = presence bits of the fields.
 struct Fields {
 	Pkt k;
 	uint32_t l3, l4, f, gates;
-	__device__ __forceinline__ uint32_t eth0() const { return r16(k, 12); }
-	__device__ __forceinline__ uint32_t ethx() const { return r16(k, (f & F_QINQ) ? 20u : 16u); }
-	__device__ __forceinline__ uint32_t vid0() const { return r16(k, 14) & 0xff0fu; }
-	__device__ __forceinline__ uint32_t pcp0() const { return (r16(k, 14) & 0xffu) >> 5; }
-	__device__ __forceinline__ uint32_t vidx() const
-	{
-		return r16(k, (f & F_QINQ) ? 18u : 14u) & 0xff0fu;
-	}
-	__device__ __forceinline__ uint32_t dmac0() const { return r32(k, 0); }
-	__device__ __forceinline__ uint32_t dmac1() const { return r16(k, 4); }
-	__device__ __forceinline__ uint32_t proto() const
-	{
-		return (f & F_IPV4) ? rb(k, l3 + 9) : rb(k, l3 + 6);
-	}
-	__device__ __forceinline__ uint32_t dscp() const
-	{
-		return (f & F_IPV4) ? (rb(k, l3 + 1) >> 2) : ((be32(k, l3) & 0x0fc00000u) >> 22);
-	}
-	__device__ __forceinline__ uint32_t ports() const
-	{
-		return (f & (F_UDP | F_TCP)) ? r32(k, l4) : 0u;
-	}
-	__device__ __forceinline__ uint32_t sip() const { return r32(k, l3 + 12); }
-	__device__ __forceinline__ uint32_t dip() const { return r32(k, l3 + 16); }
-	// word i of the IPv6 source (src) or destination address
-	__device__ __forceinline__ uint32_t a6(bool src, uint32_t i) const
-	{
-		return r32(k, l3 + (src ? 8u : 24u) + 4u * i);
-	}
-	__device__ __forceinline__ uint32_t spi() const
-	{
-		return (f & F_AH) ? r32(k, l4 + 4) : r32(k, l4);
-	}
 };
+
+// Where the key words of a term kind sit (verify_pmr_<term>,
+// odp_classification.c:931-1357): 4-byte little-endian words at
+// base + add, or base + alt when the lane's flags have `altf`
+// (QinQ outer tag, IPv4 vs IPv6 next-header, AH vs ESP SPI); base is the
+// frame start, L3 or L4.  The term's mask words cut each word down to the
+// field (e.g. 0xffff for a 16-bit field), so every kind but LEN, PCP and
+// DSCP is "read words, AND mask".  gate: presence bits the packet needs.
+enum { FB_FRAME = 0, FB_L3 = 1, FB_L4 = 2 };
+struct FDesc {
+	uint32_t base, add, alt, altf, gate;
+};
+
+__device__ __forceinline__ FDesc fdesc(uint32_t kind, uint32_t toff)
+{
+	FDesc d = { FB_FRAME, 0u, 0u, 0u, 0u };
+	switch (kind) {
+	case MI_K_ETH0: d = { FB_FRAME, 12u, 12u, 0u, G_ETH }; break;
+	case MI_K_ETHX: d = { FB_FRAME, 16u, 20u, F_QINQ, G_VLANX }; break;
+	case MI_K_VID0: d = { FB_FRAME, 14u, 14u, 0u, G_VLAN0 }; break;
+	case MI_K_VIDX: d = { FB_FRAME, 14u, 18u, F_QINQ, G_VLANX }; break;
+	case MI_K_DMAC: d = { FB_FRAME, 0u, 0u, 0u, G_ETH }; break;
+	case MI_K_PROTO: d = { FB_L3, 6u, 9u, F_IPV4, G_V4 | G_V6 }; break;
+	case MI_K_UDP_DPORT:
+	case MI_K_UDP_SPORT: d = { FB_L4, 0u, 0u, 0u, G_UDP }; break;
+	case MI_K_TCP_DPORT:
+	case MI_K_TCP_SPORT: d = { FB_L4, 0u, 0u, 0u, G_TCP }; break;
+	case MI_K_SIP: d = { FB_L3, 12u, 12u, 0u, G_V4 }; break;
+	case MI_K_DIP: d = { FB_L3, 16u, 16u, 0u, G_V4 }; break;
+	case MI_K_SIP6: d = { FB_L3, 8u, 8u, 0u, G_V6 }; break;
+	case MI_K_DIP6: d = { FB_L3, 24u, 24u, 0u, G_V6 }; break;
+	case MI_K_SPI: d = { FB_L4, 0u, 4u, F_AH, G_SPI }; break;
+	case MI_K_CUSTOM_FRAME: d = { FB_FRAME, toff, toff, 0u, ~0u }; break;
+	case MI_K_CUSTOM_L3: d = { FB_L3, toff, toff, 0u, G_L3OK }; break;
+	default: break;
+	}
+	return d;
+}
+
+__device__ __forceinline__ bool kind_special(uint32_t kind)
+{
+	return kind == MI_K_LEN || kind == MI_K_PCP0 || kind == MI_K_DSCP || kind == MI_K_NEVER ||
+	       kind == MI_K_ALWAYS;
+}
+
+// LEN / PCP / DSCP values and presence (NEVER: absent, ALWAYS: present)
+__device__ __forceinline__ bool special_value(uint32_t kind, const Fields &x, uint32_t &v)
+{
+	const uint32_t g = x.gates;
+	if (kind == MI_K_LEN) {
+		v = x.k.len;
+		return true;
+	}
+	if (kind == MI_K_PCP0) {
+		v = (r16(x.k, 14) & 0xffu) >> 5;
+		return (g & G_VLAN0) != 0u;
+	}
+	if (kind == MI_K_DSCP) {
+		v = (x.f & F_IPV4) ? (rb(x.k, x.l3 + 1) >> 2)
+				   : ((be32(x.k, x.l3) & 0x0fc00000u) >> 22);
+		return (g & (G_V4 | G_V6)) != 0u;
+	}
+	v = 0;
+	return kind == MI_K_ALWAYS;
+}
+
+// Byte offset of a kind's first key word in the lane's frame, and whether the
+// packet has the field (custom kinds: the frame must extend past
+// offset + size, verify_pmr_custom_*).
+__device__ __forceinline__ uint32_t field_off(const FDesc &d, uint32_t kind, uint32_t size,
+					      const Fields &x, bool &present)
+{
+	const uint32_t base = d.base == FB_L3 ? x.l3 : (d.base == FB_L4 ? x.l4 : 0u);
+	const uint32_t o = base + ((x.f & d.altf) ? d.alt : d.add);
+	present = d.gate == ~0u || (x.gates & d.gate) != 0u;
+	if (kind == MI_K_CUSTOM_FRAME || kind == MI_K_CUSTOM_L3)
+		present = present && !(x.k.len <= o + size);
+	return o;
+}
 
 __device__ __forceinline__ uint32_t gates_of(const Parsed &p)
 {
@@ -676,94 +722,23 @@ __device__ __forceinline__ bool term_ok(cword_t prog, uint32_t &q, const Pkt &k,
 {
 	const uint32_t op = prog[q];
 	const uint32_t kind = op & 0xffu;
-	const uint32_t g = x.gates;
-	if (kind == MI_K_CUSTOM_FRAME || kind == MI_K_CUSTOM_L3) {
-		const uint32_t sz = (op >> 8) & 0xffu;
-		const uint32_t nw = (op >> 16) & 0xffu;
-		const uint32_t toff = prog[q + 1];
-		uint32_t o = toff;
-		bool ok = true;
-		if (kind == MI_K_CUSTOM_L3) {
-			ok = (g & G_L3OK) != 0;
-			o = p.l3 + toff;
-		}
-		// verify_pmr_custom_*: "packet_len <= offset + val_sz" -> no match (u32 math)
-		ok = ok && !(k.len <= o + sz);
-		if (ok) {
-			for (uint32_t i = 0; i < nw; ++i)
-				ok = ok && eq1(r32(k, o + 4u * i), prog[q + 2 + 2 * i], prog[q + 3 + 2 * i]);
-		}
-		q += 2u + 2u * nw;
+	const uint32_t sz = (op >> 8) & 0xffu;
+	const uint32_t nw = (op >> 16) & 0xffu;
+	if (kind_special(kind)) {
+		uint32_t v;
+		const bool ok = special_value(kind, x, v) &&
+				(kind == MI_K_ALWAYS || eq1(v, prog[q + 1], prog[q + 2]));
+		q += 1u + 2u * nw;
 		return ok;
 	}
-	const uint32_t m0 = prog[q + 1];
-	const uint32_t v0 = prog[q + 2];
+	const bool custom = kind == MI_K_CUSTOM_FRAME || kind == MI_K_CUSTOM_L3;
+	const FDesc d = fdesc(kind, custom ? prog[q + 1] : 0u);
+	const uint32_t q0 = q + (custom ? 2u : 1u);
 	bool ok;
-	switch (kind) {
-	case MI_K_LEN:
-		ok = eq1(k.len, m0, v0);
-		break;
-	case MI_K_ETH0:
-		ok = (g & G_ETH) && eq1(x.eth0(), m0, v0);
-		break;
-	case MI_K_ETHX:
-		ok = (g & G_VLANX) && eq1(x.ethx(), m0, v0);
-		break;
-	case MI_K_VID0:
-		ok = (g & G_VLAN0) && eq1(x.vid0(), m0, v0);
-		break;
-	case MI_K_VIDX:
-		ok = (g & G_VLANX) && eq1(x.vidx(), m0, v0);
-		break;
-	case MI_K_PCP0:
-		ok = (g & G_VLAN0) && eq1(x.pcp0(), m0, v0);
-		break;
-	case MI_K_DMAC:
-		ok = (g & G_ETH) && eq1(x.dmac0(), m0, v0) && eq1(x.dmac1(), prog[q + 3], prog[q + 4]);
-		q += 2;
-		break;
-	case MI_K_PROTO:
-		ok = (g & (G_V4 | G_V6)) && eq1(x.proto(), m0, v0);
-		break;
-	case MI_K_DSCP:
-		ok = (g & (G_V4 | G_V6)) && eq1(x.dscp(), m0, v0);
-		break;
-	case MI_K_UDP_DPORT:
-	case MI_K_UDP_SPORT:
-		ok = (g & G_UDP) && eq1(x.ports(), m0, v0);
-		break;
-	case MI_K_TCP_DPORT:
-	case MI_K_TCP_SPORT:
-		ok = (g & G_TCP) && eq1(x.ports(), m0, v0);
-		break;
-	case MI_K_SIP:
-		ok = (g & G_V4) && eq1(x.sip(), m0, v0);
-		break;
-	case MI_K_DIP:
-		ok = (g & G_V4) && eq1(x.dip(), m0, v0);
-		break;
-	case MI_K_SIP6:
-	case MI_K_DIP6: {
-		// element-wise select: a pointer select would put the arrays on the stack
-		const bool src = kind == MI_K_SIP6;
-		ok = (g & G_V6) && eq1(x.a6(src, 0), m0, v0) &&
-		     eq1(x.a6(src, 1), prog[q + 3], prog[q + 4]) &&
-		     eq1(x.a6(src, 2), prog[q + 5], prog[q + 6]) &&
-		     eq1(x.a6(src, 3), prog[q + 7], prog[q + 8]);
-		q += 6;
-		break;
-	}
-	case MI_K_SPI:
-		ok = (g & G_SPI) && eq1(x.spi(), m0, v0);
-		break;
-	case MI_K_ALWAYS:
-		ok = true;
-		break;
-	default:   // MI_K_NEVER (LD_VNI)
-		ok = false;
-		break;
-	}
-	q += 3;
+	const uint32_t o = field_off(d, kind, sz, x, ok);
+	for (uint32_t i = 0; i < nw; ++i)
+		ok = ok && eq1(r32(k, o + 4u * i), prog[q0 + 2u * i], prog[q0 + 2u * i + 1u]);
+	q = q0 + 2u * nw;
 	return ok;
 }
 
@@ -796,115 +771,54 @@ template <typename D>
 __device__ __forceinline__ bool bv_key(const D &cr, const Pkt &k, const Parsed &p, const Fields &x,
 				       uint32_t key[4])
 {
-	const uint32_t kind = cr(0);
-	const uint32_t m0 = cr(5);
-	const uint32_t g = x.gates;
-	key[1] = key[2] = key[3] = 0;
-	switch (kind) {
-	case MI_K_LEN:
-		key[0] = k.len & m0;
-		return true;
-	case MI_K_ETH0:
-		key[0] = x.eth0() & m0;
-		return g & G_ETH;
-	case MI_K_ETHX:
-		key[0] = x.ethx() & m0;
-		return g & G_VLANX;
-	case MI_K_VID0:
-		key[0] = x.vid0() & m0;
-		return g & G_VLAN0;
-	case MI_K_VIDX:
-		key[0] = x.vidx() & m0;
-		return g & G_VLANX;
-	case MI_K_PCP0:
-		key[0] = x.pcp0() & m0;
-		return g & G_VLAN0;
-	case MI_K_DMAC:
-		key[0] = x.dmac0() & m0;
-		key[1] = x.dmac1() & cr(6);
-		return g & G_ETH;
-	case MI_K_PROTO:
-		key[0] = x.proto() & m0;
-		return g & (G_V4 | G_V6);
-	case MI_K_DSCP:
-		key[0] = x.dscp() & m0;
-		return g & (G_V4 | G_V6);
-	case MI_K_UDP_DPORT:
-	case MI_K_UDP_SPORT:
-		key[0] = x.ports() & m0;
-		return g & G_UDP;
-	case MI_K_TCP_DPORT:
-	case MI_K_TCP_SPORT:
-		key[0] = x.ports() & m0;
-		return g & G_TCP;
-	case MI_K_SIP:
-		key[0] = x.sip() & m0;
-		return g & G_V4;
-	case MI_K_DIP:
-		key[0] = x.dip() & m0;
-		return g & G_V4;
-	case MI_K_SIP6:
-	case MI_K_DIP6: {
-		const bool src = kind == MI_K_SIP6;
-		key[0] = x.a6(src, 0) & m0;
-		key[1] = x.a6(src, 1) & cr(6);
-		key[2] = x.a6(src, 2) & cr(7);
-		key[3] = x.a6(src, 3) & cr(8);
-		return g & G_V6;
+	const uint32_t kind = cr(0), nk = cr(1);
+	key[0] = key[1] = key[2] = key[3] = 0;
+	if (kind_special(kind)) {
+		uint32_t v;
+		const bool pr = special_value(kind, x, v);
+		key[0] = v & cr(5);
+		return pr;
 	}
-	case MI_K_SPI:
-		key[0] = x.spi() & m0;
-		return g & G_SPI;
-	case MI_K_CUSTOM_FRAME:
-	case MI_K_CUSTOM_L3: {
-		const uint32_t toff = cr(3), sz = cr(4), nk = cr(1);
-		uint32_t o = toff;
-		bool ok = true;
-		if (kind == MI_K_CUSTOM_L3) {
-			ok = (g & G_L3OK) != 0;
-			o = p.l3 + toff;
-		}
-		ok = ok && !(k.len <= o + sz);
-		key[0] = 0;
-		if (ok) {
-			key[0] = r32(k, o) & m0;
-			if (nk > 1)
-				key[1] = r32(k, o + 4) & cr(6);
-			if (nk > 2) {
-				key[2] = r32(k, o + 8) & cr(7);
-				key[3] = r32(k, o + 12) & cr(8);
-			}
-		}
-		return ok;
+	const FDesc d = fdesc(kind, cr(3));
+	bool present;
+	const uint32_t o = field_off(d, kind, cr(4), x, present);
+	key[0] = r32(k, o) & cr(5);
+	if (nk > 1)
+		key[1] = r32(k, o + 4u) & cr(6);
+	if (nk > 2) {
+		key[2] = r32(k, o + 8u) & cr(7);
+		key[3] = r32(k, o + 12u) & cr(8);
 	}
-	default:
-		key[0] = 0;
-		return false;
-	}
+	return present;
 }
 
-// Probe a class's open-addressing table for the lane's key; returns the
-// slot's value (row index / first rule) or `miss` when the key is absent.
+// Probe a class's open-addressing table for the key of every lane in `act`;
+// returns the slot's value (row index / first rule) or `miss` when the key
+// is absent.  The probe loop runs until no lane of the wave is still
+// searching; per-lane state lives in VGPRs and is updated by selects.
 template <typename T>
 __device__ __forceinline__ uint32_t bv_probe(T H, uint32_t tbl, uint32_t tmask, uint32_t nk,
-					     const uint32_t key[4], uint32_t miss)
+					     const uint32_t key[4], bool act, uint32_t miss)
 {
-	uint32_t h = bv_hash(key) & tmask;
+	uint32_t h = bv_hash(key) & tmask, val = miss;
+	uint32_t searching = act ? 1u : 0u;
 	for (uint32_t probe = 0; probe <= tmask; ++probe) {
-		const uint32_t s = tbl + h * (nk + 1u);
-		const uint32_t rw = H[s + nk];
-		if (rw == BV_EMPTY)
+		if (__ballot(searching != 0u) == 0ull)
 			break;
-		bool eq = H[s] == key[0];
+		const uint32_t sl = tbl + h * (nk + 1u);
+		const uint32_t rw = H[sl + nk];
+		bool eq = H[sl] == key[0];
 		if (nk > 1)
-			eq = eq && H[s + 1] == key[1];
+			eq = eq && H[sl + 1] == key[1];
 		if (nk > 2)
-			eq = eq && H[s + 2] == key[2] && H[s + 3] == key[3];
-		if (eq)
-			return rw;
+			eq = eq && H[sl + 2] == key[2] && H[sl + 3] == key[3];
+		const bool empty = rw == BV_EMPTY;
+		const bool found = searching != 0u && !empty && eq;
+		val = found ? rw : val;
+		searching = (searching != 0u && !empty && !eq) ? 1u : 0u;
 		h = (h + 1u) & tmask;
 	}
-	return miss;
+	return val;
 }
 
 // Bit-vector evaluation of one CoS for the lanes in `act`.  `blk` reads the
@@ -913,7 +827,8 @@ __device__ __forceinline__ uint32_t bv_probe(T H, uint32_t tbl, uint32_t tmask, 
 // done = true and the rule's destination CoS / mark in nxt / nmark.
 template <typename D, typename T>
 __device__ __forceinline__ void bv_eval(const D &blk, T H, bool act, const Pkt &k, const Parsed &p,
-					const Fields &x, bool &done, uint32_t &nxt, uint32_t &nmark, bool &nleaf)
+					const Fields &x, uint32_t &hit, uint32_t &nxt, uint32_t &nmark,
+					uint32_t &nleaf)
 {
 	const uint32_t Wd = blk(0), ncls = blk(1), alive = blk(2), res = blk(3);
 	uint32_t first = BV_NONE;
@@ -923,9 +838,7 @@ __device__ __forceinline__ void bv_eval(const D &blk, T H, bool act, const Pkt &
 		uint32_t key[4];
 		const bool present = bv_key(cr, k, p, x, key);
 		const uint32_t r0 = cr(2);
-		first = r0;
-		if (act && present)
-			first = bv_probe(H, cr(10), cr(9), cr(1), key, r0);
+		first = bv_probe(H, cr(10), cr(9), cr(1), key, act && present, r0);
 	} else {
 		uint32_t ridx[BV_MAX_CLS];
 #pragma unroll
@@ -935,46 +848,40 @@ __device__ __forceinline__ void bv_eval(const D &blk, T H, bool act, const Pkt &
 				const D cr = blk.at(4u + BV_CLS_WORDS * kc);
 				uint32_t key[4];
 				const bool present = bv_key(cr, k, p, x, key);
-				uint32_t row = 0;
-				if (act && present)
-					row = bv_probe(H, cr(10), cr(9), cr(1), key, 0u);
+				const uint32_t row = bv_probe(H, cr(10), cr(9), cr(1), key, act && present, 0u);
 				ridx[kc] = cr(11) + row * Wd;
 			}
 		}
-		bool found = false;
+		uint32_t want = act ? 1u : 0u;
 		for (uint32_t w = 0; w < Wd; ++w) {
-			if (__ballot(act && !found) == 0ull)
+			if (__ballot(want != 0u) == 0ull)
 				break;
-			if (act && !found) {
-				uint32_t acc = H[alive + w];
+			uint32_t acc = H[alive + w];
 #pragma unroll
-				for (uint32_t kc = 0; kc < BV_MAX_CLS; ++kc)
-					if (kc < ncls)
-						acc &= H[ridx[kc] + w];
-				if (acc) {
-					found = true;
-					first = w * 32u + (uint32_t)__builtin_ctz(acc);
-				}
-			}
+			for (uint32_t kc = 0; kc < BV_MAX_CLS; ++kc)
+				if (kc < ncls)
+					acc &= H[ridx[kc] + w];
+			const bool f = want != 0u && acc != 0u;
+			first = f ? w * 32u + (uint32_t)__builtin_ctz(acc) : first;
+			want = (want != 0u && acc == 0u) ? 1u : 0u;
 		}
 	}
-	if (act && first != BV_NONE) {
-		const uint32_t rw = H[res + first];
-		nxt = rw & 0xffu;
-		nleaf = (rw >> 8) & 1u;
-		nmark = rw >> 16;
-		done = true;
-	}
+	const bool h = act && first != BV_NONE;
+	const uint32_t rw = H[res + (h ? first : 0u)];
+	nxt = h ? (rw & 0xffu) : nxt;
+	nleaf = h ? ((rw >> 8) & 1u) : nleaf;
+	nmark = h ? (rw >> 16) : nmark;
+	hit = h ? 1u : hit;
 }
 
 // Linear scan of one wave-uniform CoS's rule records for the lanes in
 // `grp` (verify_pmr over cos->pmr[] in order, first match wins).
 __device__ __forceinline__ void linear_scan(cword_t prog, uint32_t rec0, uint32_t nr, bool grp,
 					    const Pkt &k, const Parsed &p, const Fields &x,
-					    bool &done, uint32_t &nxt, uint32_t &nmark)
+					    uint32_t &done, uint32_t &nxt, uint32_t &nmark)
 {
 	for (uint32_t r = 0; r < nr; ++r) {
-		const bool cand = grp && !done;
+		const bool cand = grp && done == 0u;
 		if (__ballot(cand) == 0ull)
 			break;
 		const uint32_t base = (rec0 + r) * REC_WORDS;
@@ -997,11 +904,9 @@ __device__ __forceinline__ void linear_scan(cword_t prog, uint32_t rec0, uint32_
 				ok = term_ok(prog, q, k, p, x) && ok;
 			}
 		}
-		if (ok) {
-			nxt = w1 & 0xffu;
-			nmark = w0 >> 16;
-			done = true;
-		}
+		nxt = ok ? (w1 & 0xffu) : nxt;
+		nmark = ok ? (w0 >> 16) : nmark;
+		done = ok ? 1u : done;
 	}
 }
 // Diagnostic build only (-DDIAG_STAMPS): per-phase cycle sums per wave,
@@ -1163,8 +1068,7 @@ __device__ __forceinline__ void wave_lds_sync()
 extern __shared__ uint32_t s_dyn[];
 
 template <bool LT, bool DIV>
-__global__ __launch_bounds__(BLOCK, DIV ? MIN_WAVES_PER_EU - 1 : MIN_WAVES_PER_EU) void
-mi_cls_kernel(KArgs a)
+__global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_EU) void mi_cls_kernel(KArgs a)
 {
 	__shared__ uint32_t s_win[WAVES_PER_BLOCK * RS * WROWS];
 	__shared__ uint32_t s_cnt[MAX_STATS_COS];
@@ -1308,132 +1212,102 @@ mi_cls_kernel(KArgs a)
 #endif
 
 		// ---- select the starting CoS (cls_select_cos, odp_classification.c:1694-1726)
-		int32_t cur = -1;
-		bool pend = false;
-		uint32_t outcome = MI_CLS_OUT_ENQ;
-		if (!valid) {
-			outcome = MI_CLS_OUT_DISCARD;
-		} else if (p.ret < 0) {
-			outcome = MI_CLS_OUT_PARSE_DROP;
-		} else if (p.err) {
-			cur = err_cos;
-		} else {
-			cur = def_cos;
-			pend = def_cos >= 0 && def_valid;
-		}
+		// Per-lane state is kept in integers updated by selects: bools live
+		// across the descent loop would become lane masks merged at every
+		// join (and spill SGPRs).
+		const bool ok_parse = valid && p.ret >= 0;
+		const bool perr = p.err != 0u;
+		int32_t cur = perr ? err_cos : def_cos;
+		uint32_t pend = (ok_parse && !perr && def_cos >= 0 && def_valid) ? 1u : 0u;
 
-		STAMP(2);   // parsed, start CoS selected, fields loaded
-		// ---- CoS descent (match_pmr_cos, :1624-1667).  Each round moves every
-		// pending lane one hop: lanes on a bit-vector CoS evaluate it in
-		// parallel (uniformly when they all sit on one CoS -- scalar loads --
-		// or each on its own CoS); lanes on a linear-scan CoS are served one
-		// CoS per round, wave-uniform, with the rule words in SGPRs.
-		uint32_t hops = 0, mark = 0;
-		bool matched = false, loop = false;
+		STAMP(2);   // parsed, start CoS selected
+		// ---- CoS descent (match_pmr_cos, :1624-1667).  Each round moves
+		// pending lanes one hop: the CoS of the first pending lane is
+		// evaluated by every lane sitting on it (bit-vector or linear engine,
+		// the CoS's words in SGPRs); in tree programs (DIV) lanes on other
+		// bit-vector CoS evaluate their own blocks in the same round.
+		uint32_t hops = 0, mark = 0, matched = 0, loop = 0;
 		for (;;) {
-			const unsigned long long pm = __ballot(pend);
+			const unsigned long long pm = __ballot(pend != 0u);
 			if (pm == 0ull)
 				break;
-			bool done = false, nleaf = false, extra = false;
-			uint32_t nxt = 0, nmark = 0;
-			bool act = pend;
+			uint32_t hit = 0, nleaf = 0, nxt = 0, nmark = 0, handled = 0;
+			bool act = pend != 0u;
 			if constexpr (DIV) {
-				// lanes on different CoS: every lane on a bit-vector CoS
-				// evaluates its own block (gathers from the hot region), lanes
-				// on a CoS without rules finish; the rest go to the uniform
-				// engine below, one CoS per round
 				const int32_t c0 = __builtin_amdgcn_readlane(cur, (int)__builtin_ctzll(pm));
-				if (__ballot(pend && cur != c0) != 0ull) {
-					const uint32_t ci = COS_WORDS * (uint32_t)(pend ? cur : c0);
+				if (__ballot(pend != 0u && cur != c0) != 0ull) {
+					const uint32_t ci = COS_WORDS * (uint32_t)(pend != 0u ? cur : c0);
 					const uint32_t my_nr = H[ci + C_NR];
 					const uint32_t my_bv = H[ci + C_BV];
-					const bool empty = pend && my_nr == 0u;
-					const bool bvl = pend && my_nr != 0u && my_bv != 0u;
+					const bool empty = pend != 0u && my_nr == 0u;
+					const bool bvl = pend != 0u && my_nr != 0u && my_bv != 0u;
 					if (__ballot(bvl))
-						bv_eval(DescL<hot_t>{ H, my_bv }, H, bvl, k, p, x, done, nxt,
-							nmark, nleaf);
-					extra = bvl || empty;
-					act = pend && !extra;
+						bv_eval(DescL<hot_t>{ H, my_bv }, H, bvl, k, p, x, hit, nxt, nmark,
+							nleaf);
+					handled = (bvl || empty) ? 1u : 0u;
+					act = pend != 0u && handled == 0u;
 				}
 			}
-			// uniform engine: the CoS of the first lane in `act`, evaluated by
-			// every lane sitting on it with the CoS's words in SGPRs
-			bool grp = false;
+			uint32_t grp = 0;
 			const unsigned long long am = __ballot(act);
 			if (am) {
 				const int32_t c1 = __builtin_amdgcn_readlane(cur, (int)__builtin_ctzll(am));
-				grp = act && cur == c1;
+				const bool g = act && cur == c1;
+				grp = g ? 1u : 0u;
 				const cword_t ce = hc + COS_WORDS * (uint32_t)c1;
 				const uint32_t nr = ce[C_NR], bv = ce[C_BV];
 				if (bv != 0u && nr != 0u)
-					bv_eval(DescU{ hc + bv }, H, grp, k, p, x, done, nxt, nmark, nleaf);
+					bv_eval(DescU{ hc + bv }, H, g, k, p, x, hit, nxt, nmark, nleaf);
 				else
-					linear_scan(prog, ce[C_REC0], nr, grp, k, p, x, done, nxt, nmark);
+					linear_scan(prog, ce[C_REC0], nr, g, k, p, x, hit, nxt, nmark);
 			}
-			const bool proc = extra || grp;
-			if (proc) {
-				if (done) {
-					cur = (int32_t)nxt;
-					mark = nmark;
-					matched = true;
-					++hops;
-					if (stats_on && stats_bit(a, nxt))
-						atomicAdd(&s_cnt[nxt], 1u);
-					if (hops > max_hops) {
-						loop = true;
-						pend = false;
-					} else if (nleaf) {
-						pend = false;   // no rules at the destination
-					}
-				} else {
-					pend = false;
-				}
+			const uint32_t proc = handled | grp;
+			const uint32_t take = proc & hit;
+			cur = take ? (int32_t)nxt : cur;
+			mark = take ? nmark : mark;
+			matched |= take;
+			hops += take;
+			const uint32_t lp = (take != 0u && hops > max_hops) ? 1u : 0u;
+			loop |= lp;
+			// still pending: a rule matched, under the hop limit, and the
+			// destination CoS has rules
+			pend = proc ? ((take != 0u && lp == 0u && nleaf == 0u) ? 1u : 0u) : pend;
+			if (stats_on) {
+				if (take != 0u && stats_bit(a, nxt))
+					atomicAdd(&s_cnt[nxt], 1u);
 			}
 		}
 
 		STAMP(3);   // descent done
 		// ---- final CoS -> outcome / queue (_odp_cls_classify_packet, :1742-1771)
-		uint32_t flags = p.flags, out_mark = 0, queue = 0, cos_idx = 0xFFu;
-		if (matched && !loop) {
-			flags &= ~F_CLS_MARK;
-			if (mark) {
-				flags |= F_CLS_MARK;
-				out_mark = mark;
-			}
+		const bool mk = matched != 0u && loop == 0u;
+		const uint32_t flags = mk ? ((p.flags & ~F_CLS_MARK) | (mark ? F_CLS_MARK : 0u)) : p.flags;
+		const uint32_t out_mark = (mk && mark) ? mark : 0u;
+		const bool live = ok_parse && loop == 0u;
+		// error CoS, the CoS the descent ended on, or the default CoS
+		const bool to_cur = !perr && matched != 0u && cur != def_cos;
+		const int32_t fc = perr ? err_cos : (to_cur ? cur : def_cos);
+		if (stats_on) {
+			if (live && !to_cur && fc >= 0 && stats_bit(a, (uint32_t)fc))
+				atomicAdd(&s_cnt[fc], 1u);
 		}
-		if (loop) {
-			outcome = MI_CLS_OUT_LOOP;
-			hops = 0xFFu;
-		} else if (valid && p.ret >= 0) {
-			int32_t fc;
-			if (p.err) {
-				fc = err_cos;
-				if (stats_on && fc >= 0 && stats_bit(a, (uint32_t)fc))
-					atomicAdd(&s_cnt[fc], 1u);
-			} else if (matched && cur != def_cos) {
-				fc = cur;
-			} else {
-				fc = def_cos;
-				if (stats_on && fc >= 0 && stats_bit(a, (uint32_t)fc))
-					atomicAdd(&s_cnt[fc], 1u);
-			}
-			if (fc < 0) {
-				outcome = MI_CLS_OUT_DISCARD;
-			} else {
-				const uint32_t meta = H[COS_WORDS * (uint32_t)fc + C_META];
-				cos_idx = meta >> 24;
-				const uint32_t nq = (meta >> 8) & 0xffu;
-				if (meta & 0xffu) {
-					outcome = MI_CLS_OUT_COS_DROP;
-				} else {
-					outcome = MI_CLS_OUT_ENQ;
-					if (nq > 1u) {
-						uint32_t h = rss_hash(k, p, (meta >> 16) & 0xffu) & 31u;
-						queue = h % nq;
-					}
-				}
-			}
+		const uint32_t meta = H[COS_WORDS * (uint32_t)max(fc, 0) + C_META];
+		const bool have = live && fc >= 0;
+		const bool drop = (meta & 0xffu) != 0u;
+		const uint32_t outcome = !valid ? MI_CLS_OUT_DISCARD
+			: (p.ret < 0 ? MI_CLS_OUT_PARSE_DROP
+			: (loop ? MI_CLS_OUT_LOOP
+			: (fc < 0 ? MI_CLS_OUT_DISCARD
+			: (drop ? MI_CLS_OUT_COS_DROP : MI_CLS_OUT_ENQ))));
+		const uint32_t cos_idx = have ? (meta >> 24) : 0xFFu;
+		const uint32_t nq = (meta >> 8) & 0xffu;
+		const bool hq = have && !drop && nq > 1u;
+		uint32_t queue = 0;
+		if (__ballot(hq) != 0ull) {
+			if (hq)
+				queue = (rss_hash(k, p, (meta >> 16) & 0xffu) & 31u) % nq;
 		}
+		hops = loop ? 0xFFu : hops;
 
 		prev_rec.x = flags;
 		prev_rec.y = (p.err & 0xffu) | ((outcome & 0xffu) << 8) | ((cos_idx & 0xffu) << 16) |
@@ -1571,6 +1445,27 @@ static int validate_tbl(const void *tbl, size_t bytes)
 	return 0;
 }
 
+// Mask word i of a term as the kernel applies it: the term's mask cut down
+// to the field's own bits in the 4-byte word the kernel reads (the kernel
+// reads every fixed field as a whole little-endian word, see fdesc()).
+static uint32_t eff_mask(const mi_term_t &t, uint32_t i)
+{
+	switch (t.kind) {
+	case MI_K_ETH0:
+	case MI_K_ETHX:
+		return t.mask[i] & 0xffffu;
+	case MI_K_VID0:
+	case MI_K_VIDX:
+		return t.mask[i] & 0xff0fu;      // VLAN ID bits of the raw TCI
+	case MI_K_PROTO:
+		return t.mask[i] & 0xffu;
+	case MI_K_DMAC:
+		return i == 1 ? (t.mask[i] & 0xffffu) : t.mask[i];
+	default:
+		return t.mask[i];
+	}
+}
+
 // words of one term in the device encoding (see "device rule program")
 static uint32_t encode_term(const mi_term_t &t, uint32_t *w)
 {
@@ -1588,7 +1483,7 @@ static uint32_t encode_term(const mi_term_t &t, uint32_t *w)
 	uint32_t nw = (t.kind == MI_K_SIP6 || t.kind == MI_K_DIP6) ? 4u : (t.kind == MI_K_DMAC ? 2u : 1u);
 	w[n++] = t.kind | ((uint32_t)t.size << 8) | (nw << 16);
 	for (uint32_t i = 0; i < nw; ++i) {
-		w[n++] = t.mask[i];
+		w[n++] = eff_mask(t, i);
 		w[n++] = t.value[i];
 	}
 	return n;
@@ -1644,7 +1539,7 @@ static bool class_of(const mi_term_t &t, ClassKey &ck)
 		ck.nkey = 1;
 	}
 	for (uint32_t i = 0; i < 4; ++i)
-		ck.mask[i] = i < ck.nkey ? t.mask[i] : 0;
+		ck.mask[i] = i < ck.nkey ? eff_mask(t, i) : 0;
 	return true;
 }
 
@@ -1962,7 +1857,7 @@ extern "C" int mi_cls_classify(mi_cls_ctx_t *c, const uint8_t *pkts, const uint3
 	const size_t lds_block = lds_static + (lt ? hot_bytes : 0);
 	const bool div = c->tree;
 	int per_cu = (int)((160u * 1024u) / lds_block);
-	const int occ = div ? MIN_WAVES_PER_EU - 1 : MIN_WAVES_PER_EU;   // waves/SIMD by VGPRs
+	const int occ = MIN_WAVES_PER_EU;   // waves/SIMD the register budget allows
 	if (per_cu > occ * 4 / WAVES_PER_BLOCK)
 		per_cu = occ * 4 / WAVES_PER_BLOCK;
 	if (per_cu_env > 0)
