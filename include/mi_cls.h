@@ -185,6 +185,20 @@ int mi_cls_classify(mi_cls_ctx_t *ctx, const uint8_t *pkts_dev, const uint32_t *
 		    const uint16_t *len_dev, uint32_t n, mi_cls_result_t *out_dev,
 		    void *stream);
 
+/* Host-memory batch (the pktio receive path, loop.c:253-384 / pcap.c:280-401):
+ * copies `bytes` of packed frames starting at pkts_host (offsets relative to
+ * it) plus the descriptors to the context's device staging buffers on its own
+ * stream, classifies, copies the n records to out_host and waits.  Host
+ * buffers from mi_cls_host_alloc() (pinned) take the DMA fast path; any
+ * other host memory is also accepted. */
+int mi_cls_classify_host(mi_cls_ctx_t *ctx, const uint8_t *pkts_host, size_t bytes,
+			 const uint32_t *off_host, const uint16_t *len_host, uint32_t n,
+			 mi_cls_result_t *out_host);
+
+/* Pinned (page-locked) host memory for staging; NULL on failure. */
+void *mi_cls_host_alloc(size_t bytes);
+void mi_cls_host_free(void *p);
+
 /* Per-CoS packet counters with the reference's per-hop counting rule
  * (odp_classification.c:1646-1647, 1721-1723): when enabled, each
  * mi_cls_classify() adds into a device array of num_cos uint64 counters

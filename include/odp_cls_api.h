@@ -12,9 +12,9 @@
  * when the first fails; destroy returns 0 / -1.  The library owns the rule
  * tables; value/mask buffers are copied at create time.
  *
- * Queue and pool handles are stored and returned, never dereferenced: the
- * classifier only needs them as opaque identities (the queue / pool
- * subsystems of ODP are outside this build's scope).
+ * Base types, queue / pool handles and odp_queue_param_t come from odp_rt.h
+ * (the runtime subset); hash-queue CoS create their queues with
+ * odp_queue_create() as the reference does (odp_classification.c:318-341).
  */
 #ifndef ODP_AMD_CLS_API_H_
 #define ODP_AMD_CLS_API_H_
@@ -23,28 +23,11 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "odp_rt.h"
+
 #ifdef __cplusplus
 extern "C" {
 #endif
-
-typedef bool odp_bool_t;
-
-/* opaque pointer-sized handles, 0 == INVALID (abi-default headers) */
-typedef struct _odp_abi_cos_t   *odp_cos_t;
-typedef struct _odp_abi_pmr_t   *odp_pmr_t;
-typedef struct _odp_abi_queue_t *odp_queue_t;
-typedef struct _odp_abi_pool_t  *odp_pool_t;
-typedef struct _odp_abi_pktio_t *odp_pktio_t;
-typedef struct _odp_abi_packet_t *odp_packet_t;
-
-#define ODP_COS_INVALID   ((odp_cos_t)0)
-#define ODP_PMR_INVALID   ((odp_pmr_t)0)
-#define ODP_QUEUE_INVALID ((odp_queue_t)0)
-#define ODP_POOL_INVALID  ((odp_pool_t)0)
-#define ODP_PKTIO_INVALID ((odp_pktio_t)0)
-#define ODP_COS_NAME_LEN  32
-
-typedef enum { ODP_SUPPORT_NO = 0, ODP_SUPPORT_YES, ODP_SUPPORT_PREFERRED } odp_support_t;
 
 /* classification.h:55-137 -- enum order is ABI */
 typedef enum {
@@ -138,19 +121,6 @@ typedef struct odp_pmr_create_opt_t {
 	uint32_t priority;
 } odp_pmr_create_opt_t;
 
-/* packet_io_types.h:124-146 */
-typedef union odp_pktin_hash_proto_t {
-	struct {
-		uint32_t ipv4_udp : 1;
-		uint32_t ipv4_tcp : 1;
-		uint32_t ipv4     : 1;
-		uint32_t ipv6_udp : 1;
-		uint32_t ipv6_tcp : 1;
-		uint32_t ipv6     : 1;
-	} proto;
-	uint32_t all_bits;
-} odp_pktin_hash_proto_t;
-
 typedef struct odp_threshold_types_t {
 	uint8_t all_bits;
 } odp_threshold_types_t;
@@ -217,34 +187,6 @@ typedef enum {
 	ODP_COS_ACTION_ENQUEUE,
 	ODP_COS_ACTION_DROP,
 } odp_cos_action_t;
-
-/* Parameters of the implementation-created hash queues.  The queue subsystem
- * is not part of this build; the struct is kept for source compatibility and
- * passed through unchanged. */
-typedef struct odp_queue_param_t {
-	int type;
-	int num_aggr;
-	uint8_t opaque[64];
-} odp_queue_param_t;
-
-typedef struct odp_pktin_vector_config_t {
-	odp_bool_t enable;
-	odp_pool_t pool;
-	uint64_t max_tmo_ns;
-	uint32_t max_size;
-} odp_pktin_vector_config_t;
-
-typedef enum {
-	ODP_AEP_TYPE_NONE = 0,
-	ODP_AEP_TYPE_IPV4_FRAG,
-	ODP_AEP_TYPE_IPV6_FRAG,
-	ODP_AEP_TYPE_CUSTOM
-} odp_aggr_enq_profile_type_t;
-
-typedef struct odp_aggr_enq_profile_t {
-	odp_aggr_enq_profile_type_t type;
-	uintptr_t param;
-} odp_aggr_enq_profile_t;
 
 typedef struct odp_red_param_t {
 	odp_bool_t enable;
@@ -340,6 +282,33 @@ long odp_amd_cls_compile(odp_pktio_t pktio, void *buf, size_t cap);
  * rule snapshot when the control plane changed since the last call. */
 int odp_amd_cls_classify(odp_pktio_t pktio, const uint8_t *pkts_dev, const uint32_t *off_dev,
 			 const uint16_t *len_dev, uint32_t n, void *out_dev, void *stream);
+
+/* Host-memory form for the pktio receive path: stage, classify, copy the
+ * records back (synchronous).  parse_only = 1 parses without classifying
+ * (classifier disabled on the pktio): records carry the parse result with
+ * outcome DISCARD (or PARSE_DROP). */
+int odp_amd_cls_classify_host(odp_pktio_t pktio, const uint8_t *pkts, size_t bytes,
+			      const uint32_t *off, const uint16_t *len, uint32_t n, void *out,
+			      int parse_only);
+
+/* Create the device context, upload the current rule snapshot and run a
+ * warm-up launch (odp_pktio_start). */
+int odp_amd_cls_prepare(odp_pktio_t pktio, int parse_only);
+
+/* Enqueue-stage counters of a (CoS, queue slot) (odp_cls_queue_stats). */
+void odp_amd_cls_queue_stats_add(uint32_t cos_index, uint32_t slot, uint64_t packets,
+				 uint64_t discards);
+
+/* cos->pool of a CoS index (pool switch of the receive path). */
+odp_pool_t odp_amd_cls_pool_of(uint32_t cos_index);
+
+/* packet_rss_hash (odp_classification.c:1773-1839) on a parsed frame;
+ * hp = bit0 ipv4, bit1 ipv6, bit2 udp, bit3 tcp. */
+uint32_t odp_amd_cls_rss_hash(const uint8_t *base, uint64_t in_flags, uint32_t l3, uint32_t l4,
+			      uint32_t hp);
+
+/* classification.h:851 */
+odp_queue_t odp_cls_hash_result(odp_cos_t cos, odp_packet_t packet);
 
 /* Map a result record's (cos index, queue slot) to the odp_queue_t handle
  * (queue_grp_tbl / cos->queue lookup of get_dest_queue, :395-405). */

@@ -1,8 +1,15 @@
 """Native build of the MI355X classification path (in-tree, no JIT cache).
 
   odp_amd/libmi_cls.so   hipcc --offload-arch=gfx950: HIP kernels + mi_cls.h C ABI
-  odp_amd/libodp_cls.so  gcc: ODP classification control plane (odp_cls_api.h),
-                         linked against libmi_cls.so (rpath $ORIGIN)
+  odp_amd/libodp_cls.so  gcc: the ODP library of this build -- classification
+                         control plane (odp_cls_api.h) + runtime subset and
+                         packet I/O (odp_rt.h), linked against libmi_cls.so
+  odp_amd/libodph.so     gcc: the ODP helper subset (odp/helper/odph_api.h)
+  examples/_bin/odp_classifier
+                         the reference's example/classifier/odp_classifier.c,
+                         compiled UNCHANGED from /root/reference against these
+                         headers and libraries (only when the reference tree is
+                         present, i.e. in the build container; the binary travels)
 """
 from __future__ import annotations
 
@@ -40,19 +47,73 @@ def build(force: bool = False, out_dir: str = PKG, defines=()) -> list[str]:
     mi_src = os.path.join(SRC, "mi_cls.hip")
     os.makedirs(out_dir, exist_ok=True)
     mi_so = os.path.join(out_dir, "libmi_cls.so")
-    odp_src = os.path.join(SRC, "odp_cls.c")
+    odp_srcs = [os.path.join(SRC, f) for f in ("odp_cls.c", "odp_rt.c", "odp_pktio.c")]
     odp_so = os.path.join(out_dir, "libodp_cls.so")
+    odph_src = os.path.join(SRC, "odph.c")
+    odph_so = os.path.join(out_dir, "libodph.so")
+    rt_hdrs = hdrs + [os.path.join(INC, "odp_rt.h"), os.path.join(INC, "odp_api.h"),
+                      os.path.join(INC, "odp", "helper", "odph_api.h"),
+                      os.path.join(SRC, "odp_rt_internal.h")]
     built = []
     if force or defines or _stale(mi_so, [mi_src] + hdrs):
         _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
               "-Wall", "-I", INC] + [f"-D{d}" for d in defines] + ["-o", mi_so, mi_src])
         built.append(mi_so)
-    if force or _stale(odp_so, [odp_src, mi_so] + hdrs):
-        _run(["gcc", "-O2", "-std=c11", "-Wall", "-Wextra", "-fPIC", "-shared", "-I", INC,
-              "-o", odp_so, odp_src, "-L", out_dir, "-lmi_cls", "-Wl,-rpath,$ORIGIN",
-              "-lpthread"])
+    if force or _stale(odp_so, odp_srcs + [mi_so] + rt_hdrs):
+        _run(["gcc", "-O2", "-std=gnu11", "-Wall", "-Wextra", "-fPIC", "-shared", "-I", INC,
+              "-o", odp_so] + odp_srcs + ["-L", out_dir, "-lmi_cls", "-Wl,-rpath,$ORIGIN",
+                                          "-lpthread"])
         built.append(odp_so)
+    if force or _stale(odph_so, [odph_src, odp_so] + rt_hdrs):
+        _run(["gcc", "-O2", "-std=gnu11", "-Wall", "-Wextra", "-fPIC", "-shared", "-I", INC,
+              "-o", odph_so, odph_src, "-L", out_dir, "-lodp_cls", "-Wl,-rpath,$ORIGIN",
+              "-lpthread"])
+        built.append(odph_so)
+    if out_dir == PKG:
+        for b in (build_example(force), build_test_drivers(force)):
+            if b:
+                built.append(b)
     return built
+
+
+TEST_BIN = os.path.join(ROOT, "tests", "_bin")
+
+
+def build_test_drivers(force: bool = False):
+    """Test-only C drivers of the runtime (tests/rt/*.c -> tests/_bin/)."""
+    src = os.path.join(ROOT, "tests", "rt", "rx_driver.c")
+    if not os.path.exists(src):
+        return None
+    os.makedirs(TEST_BIN, exist_ok=True)
+    out = os.path.join(TEST_BIN, "rx_driver")
+    if not force and not _stale(out, [src, os.path.join(PKG, "libodp_cls.so"),
+                                      os.path.join(INC, "odp_rt.h")]):
+        return None
+    _run(["gcc", "-O2", "-std=gnu11", "-Wall", "-I", INC, "-o", out, src, "-L", PKG,
+          "-lodp_cls", "-Wl,-rpath,$ORIGIN/" + os.path.relpath(PKG, TEST_BIN), "-lpthread"])
+    return out
+
+
+REF_EXAMPLE = "/root/reference/example/classifier/odp_classifier.c"
+EX_BIN = os.path.join(ROOT, "examples", "_bin")
+
+
+def build_example(force: bool = False):
+    """Compile the reference's example/classifier source, unchanged, against
+    this build's odp_api.h / odph_api.h and link it with libodp_cls.so +
+    libodph.so (north-star acceptance: the example links and runs unchanged).
+    Skipped when the reference tree is absent (GPU box: the binary travels)."""
+    if not os.path.exists(REF_EXAMPLE):
+        return None
+    os.makedirs(EX_BIN, exist_ok=True)
+    out = os.path.join(EX_BIN, "odp_classifier")
+    libs = [os.path.join(PKG, "libodp_cls.so"), os.path.join(PKG, "libodph.so")]
+    if not force and not _stale(out, [REF_EXAMPLE] + libs):
+        return None
+    _run(["gcc", "-O2", "-std=gnu11", "-I", INC, "-o", out, REF_EXAMPLE, "-L", PKG,
+          "-lodph", "-lodp_cls", "-Wl,-rpath,$ORIGIN/" + os.path.relpath(PKG, EX_BIN),
+          "-lpthread"])
+    return out
 
 
 if __name__ == "__main__":

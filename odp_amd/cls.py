@@ -35,8 +35,17 @@ class PmrCreateOpt(C.Structure):
                 ("priority", C.c_uint32)]
 
 
+class SchedParam(C.Structure):
+    _fields_ = [("prio", C.c_int), ("sync", C.c_int), ("group", C.c_int),
+                ("lock_count", C.c_uint32)]
+
+
 class QueueParam(C.Structure):
-    _fields_ = [("type", C.c_int), ("num_aggr", C.c_int), ("opaque", C.c_uint8 * 64)]
+    """odp_queue_param_t (queue_types.h:249-349)."""
+    _fields_ = [("type", C.c_int), ("enq_mode", C.c_int), ("deq_mode", C.c_int),
+                ("sched", SchedParam), ("order", C.c_int), ("nonblocking", C.c_int),
+                ("context", C.c_void_p), ("context_len", C.c_uint32), ("size", C.c_uint32),
+                ("num_aggr", C.c_uint32), ("aggr", C.c_void_p)]
 
 
 class _QP(C.Structure):

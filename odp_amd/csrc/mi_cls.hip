@@ -1348,6 +1348,14 @@ struct mi_cls_ctx {
 	int stats_on;
 	uint32_t stats_mask[8];
 	int num_cu;
+	// host-batch staging (mi_cls_classify_host)
+	hipStream_t stream;
+	uint8_t *d_pk;
+	size_t pk_cap;
+	uint32_t *d_off;
+	uint16_t *d_len;
+	mi_cls_result_t *d_out;
+	uint32_t n_cap;
 };
 
 #define HIP_OK(x) do { if ((x) != hipSuccess) return -EIO; } while (0)
@@ -1402,6 +1410,12 @@ extern "C" int mi_cls_ctx_destroy(mi_cls_ctx_t *c)
 		(void)hipFree(c->d_dev);
 	if (c->d_stats)
 		(void)hipFree(c->d_stats);
+	if (c->stream)
+		(void)hipStreamDestroy(c->stream);
+	(void)hipFree(c->d_pk);
+	(void)hipFree(c->d_off);
+	(void)hipFree(c->d_len);
+	(void)hipFree(c->d_out);
 	free(c);
 	return 0;
 }
@@ -1893,6 +1907,76 @@ extern "C" int mi_cls_classify(mi_cls_ctx_t *c, const uint8_t *pkts, const uint3
 	}
 #endif
 	return 0;
+}
+
+// Host-memory batch: stage through device buffers owned by the context on its
+// own stream (grown geometrically, kept across calls), classify, copy back.
+extern "C" int mi_cls_classify_host(mi_cls_ctx_t *c, const uint8_t *pkts, size_t bytes,
+				    const uint32_t *off, const uint16_t *len, uint32_t n,
+				    mi_cls_result_t *out)
+{
+	if (!c || !c->loaded)
+		return -EINVAL;
+	if (n == 0)
+		return 0;
+	if (!pkts || !off || !len || !out)
+		return -EINVAL;
+	// every frame must lie inside the staged bytes (the kernel reads up to
+	// the next 16-byte boundary after a frame; the staging buffer is padded)
+	for (uint32_t i = 0; i < n; ++i)
+		if ((size_t)off[i] + len[i] > bytes)
+			return -EINVAL;
+	HIP_OK(hipSetDevice(c->device));
+	if (!c->stream)
+		HIP_OK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+	const size_t need = bytes + 64;
+	if (need > c->pk_cap) {
+		(void)hipFree(c->d_pk);
+		c->d_pk = nullptr;
+		size_t cap = need < (1u << 20) ? (1u << 20) : need + need / 2;
+		if (hipMalloc((void **)&c->d_pk, cap) != hipSuccess)
+			return c->pk_cap = 0, -ENOMEM;
+		HIP_OK(hipMemset(c->d_pk, 0, cap));
+		c->pk_cap = cap;
+	}
+	if (n > c->n_cap) {
+		(void)hipFree(c->d_off);
+		(void)hipFree(c->d_len);
+		(void)hipFree(c->d_out);
+		c->d_off = nullptr;
+		c->d_len = nullptr;
+		c->d_out = nullptr;
+		uint32_t cap = n < 4096u ? 4096u : n + n / 2;
+		if (hipMalloc((void **)&c->d_off, cap * sizeof(uint32_t)) != hipSuccess ||
+		    hipMalloc((void **)&c->d_len, cap * sizeof(uint16_t)) != hipSuccess ||
+		    hipMalloc((void **)&c->d_out, cap * sizeof(mi_cls_result_t)) != hipSuccess)
+			return c->n_cap = 0, -ENOMEM;
+		c->n_cap = cap;
+	}
+	hipStream_t s = c->stream;
+	HIP_OK(hipMemcpyAsync(c->d_pk, pkts, bytes, hipMemcpyHostToDevice, s));
+	HIP_OK(hipMemcpyAsync(c->d_off, off, n * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+	HIP_OK(hipMemcpyAsync(c->d_len, len, n * sizeof(uint16_t), hipMemcpyHostToDevice, s));
+	int rc = mi_cls_classify(c, c->d_pk, c->d_off, c->d_len, n, c->d_out, s);
+	if (rc)
+		return rc;
+	HIP_OK(hipMemcpyAsync(out, c->d_out, n * sizeof(mi_cls_result_t), hipMemcpyDeviceToHost, s));
+	HIP_OK(hipStreamSynchronize(s));
+	return 0;
+}
+
+extern "C" void *mi_cls_host_alloc(size_t bytes)
+{
+	void *p = nullptr;
+	if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess)
+		return nullptr;
+	return p;
+}
+
+extern "C" void mi_cls_host_free(void *p)
+{
+	if (p)
+		(void)hipHostFree(p);
 }
 
 extern "C" int mi_cls_stats_enable(mi_cls_ctx_t *c, const uint32_t mask[8])

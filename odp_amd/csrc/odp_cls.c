@@ -65,6 +65,11 @@ typedef struct {
 	odp_queue_t hq[COS_QUEUE_MAX];
 	char name[ODP_COS_NAME_LEN];
 	uint64_t stats_discards;
+	/* per-queue enqueue counters (_odp_cos_queue_stats_add,
+	 * odp_classification_internal.h:60-81), maintained by the host
+	 * enqueue stage of the receive path */
+	uint64_t q_packets[COS_QUEUE_MAX];
+	uint64_t q_discards[COS_QUEUE_MAX];
 } cos_t;
 
 typedef struct {
@@ -74,6 +79,7 @@ typedef struct {
 	int error_cos;
 	uint32_t headroom;
 	mi_cls_ctx_t *ctx;
+	mi_cls_ctx_t *pctx;      /* parse-only context (empty table) */
 	uint64_t compiled_gen;
 	void *blob;
 	size_t blob_cap;
@@ -100,6 +106,9 @@ static void free_tables(void)
 
 	if (G.cos) {
 		for (i = 0; i < G.max_cos; i++) {
+			if (G.cos[i].valid && G.cos[i].queue_group)
+				for (uint32_t j = 0; j < G.cos[i].num_queue; j++)
+					odp_queue_destroy(G.cos[i].hq[j]);
 			free(G.cos[i].pmr);
 			free(G.cos[i].linked);
 		}
@@ -329,15 +338,26 @@ odp_cos_t odp_cls_cos_create(const char *name, const odp_cls_cos_param_t *param_
 			c->queue_group = 1;
 			c->queue = ODP_QUEUE_INVALID;
 			c->hash_proto = fold_hash_proto(param.hash_proto);
-			/* implementation-created hash queues: opaque identities */
-			for (j = 0; j < param.num_queue; j++)
-				c->hq[j] = (odp_queue_t)(uintptr_t)(0x7f0000000000ull + (++G.hq_seq));
+			/* implementation-created hash queues (:310-330) */
+			for (j = 0; j < param.num_queue; j++) {
+				char hq_name[ODP_QUEUE_NAME_LEN];
+
+				snprintf(hq_name, sizeof(hq_name), "_odp_cos_hq_%u_%u", i, j);
+				c->hq[j] = odp_queue_create(hq_name, &param.queue_param);
+				if (c->hq[j] == ODP_QUEUE_INVALID) {
+					while (j--)
+						odp_queue_destroy(c->hq[j]);
+					goto out;
+				}
+			}
 		} else {
 			c->queue_group = 0;
 			c->hash_proto = 0;
 			c->queue = param.queue;
 		}
 		c->stats_discards = 0;
+		memset(c->q_packets, 0, sizeof(c->q_packets));
+		memset(c->q_discards, 0, sizeof(c->q_discards));
 		c->action = param.action;
 		c->pool = param.pool;
 		c->valid = 1;
@@ -377,6 +397,10 @@ int odp_cos_destroy(odp_cos_t h)
 	cos_t *c = get_cos(h);
 
 	if (c) {
+		/* :494-495 */
+		if (c->queue_group)
+			for (uint32_t j = 0; j < c->num_queue; j++)
+				odp_queue_destroy(c->hq[j]);
 		c->valid = 0;
 		G.gen++;
 		rc = 0;
@@ -703,6 +727,8 @@ int odp_amd_cls_pktio_destroy(odp_pktio_t h)
 		return -1;
 	if (e->ctx)
 		mi_cls_ctx_destroy(e->ctx);
+	if (e->pctx)
+		mi_cls_ctx_destroy(e->pctx);
 	free(e->blob);
 	memset(e, 0, sizeof(*e));
 	return 0;
@@ -933,6 +959,9 @@ long odp_amd_cls_compile(odp_pktio_t h, void *buf, size_t cap)
 	return r;
 }
 
+static int ensure_ctx(pktio_t *e);
+static int sync_rules(pktio_t *e, void *stream);
+
 int odp_amd_cls_classify(odp_pktio_t h, const uint8_t *pkts_dev, const uint32_t *off_dev,
 			 const uint16_t *len_dev, uint32_t n, void *out_dev, void *stream)
 {
@@ -941,41 +970,12 @@ int odp_amd_cls_classify(odp_pktio_t h, const uint8_t *pkts_dev, const uint32_t 
 
 	if (!e)
 		return -EINVAL;
-	if (!e->ctx) {
-		rc = mi_cls_ctx_create(e->gpu, &e->ctx);
-		if (rc)
-			return rc;
-	}
-	if (e->compiled_gen != G.gen) {
-		pthread_mutex_lock(&G.lock);
-		uint64_t gen = G.gen;
-		long need = compile_locked(e, NULL, 0);
-
-		if (need < 0) {
-			pthread_mutex_unlock(&G.lock);
-			return (int)need;
-		}
-		if ((size_t)need > e->blob_cap) {
-			free(e->blob);
-			e->blob = malloc((size_t)need);
-			e->blob_cap = e->blob ? (size_t)need : 0;
-			if (!e->blob) {
-				pthread_mutex_unlock(&G.lock);
-				return -ENOMEM;
-			}
-		}
-		compile_locked(e, e->blob, e->blob_cap);
-		pthread_mutex_unlock(&G.lock);
-		rc = mi_cls_rules_load(e->ctx, e->blob, (size_t)need, stream);
-		if (rc)
-			return rc;
-		int any = 0;
-
-		for (int i = 0; i < 8; i++)
-			any |= e->stats_mask[i] != 0;
-		mi_cls_stats_enable(e->ctx, any ? e->stats_mask : NULL);
-		e->compiled_gen = gen;
-	}
+	rc = ensure_ctx(e);
+	if (rc)
+		return rc;
+	rc = sync_rules(e, stream);
+	if (rc)
+		return rc;
 	return mi_cls_classify(e->ctx, pkts_dev, off_dev, len_dev, n, (mi_cls_result_t *)out_dev,
 			       stream);
 }
@@ -1017,23 +1017,25 @@ int odp_cls_cos_stats(odp_cos_t h, odp_cls_cos_stats_t *stats)
 int odp_cls_queue_stats(odp_cos_t h, odp_queue_t q, odp_cls_queue_stats_t *stats)
 {
 	cos_t *c = get_cos(h);
-	uint32_t i;
-	int found = 0;
+	uint32_t i, slot = COS_QUEUE_MAX;
 
 	if (!c || !stats)
 		return -1;
 	if (c->queue_group) {
 		for (i = 0; i < c->num_queue; i++)
-			found |= c->hq[i] == q;
-	} else {
-		found = c->queue == q;
+			if (c->hq[i] == q)
+				slot = i;
+	} else if (c->queue == q) {
+		slot = 0;
 	}
-	if (!found) {
+	if (slot == COS_QUEUE_MAX) {
 		ERR("Invalid odp_queue_t handle\n");
 		return -1;
 	}
-	/* per-queue counters are maintained by the enqueue stage (host side) */
+	/* :1871-1898: packets / discards of the enqueue stage */
 	memset(stats, 0, sizeof(*stats));
+	stats->packets = __atomic_load_n(&c->q_packets[slot], __ATOMIC_RELAXED);
+	stats->discards = __atomic_load_n(&c->q_discards[slot], __ATOMIC_RELAXED);
 	return 0;
 }
 
@@ -1133,4 +1135,213 @@ size_t odp_amd_cls_abi_size(int which)
 	case 105: return offsetof(odp_cls_cos_param_t, hash_proto);
 	default: return 0;
 	}
+}
+
+/* ------------------------------------------------ receive-path host side */
+
+/* _odp_cos_queue_stats_add (odp_classification_internal.h:60-81) */
+void odp_amd_cls_queue_stats_add(uint32_t cos_index, uint32_t slot, uint64_t packets,
+				 uint64_t discards)
+{
+	if (!G.init || cos_index >= G.max_cos || slot >= COS_QUEUE_MAX)
+		return;
+	cos_t *c = &G.cos[cos_index];
+
+	if (packets)
+		__atomic_fetch_add(&c->q_packets[slot], packets, __ATOMIC_RELAXED);
+	if (discards)
+		__atomic_fetch_add(&c->q_discards[slot], discards, __ATOMIC_RELAXED);
+}
+
+/* cos->pool of the final CoS (_odp_cls_classify_packet, :1760-1764) */
+odp_pool_t odp_amd_cls_pool_of(uint32_t cos_index)
+{
+	if (!G.init || cos_index >= G.max_cos)
+		return ODP_POOL_INVALID;
+	return G.cos[cos_index].pool;
+}
+
+static int ensure_ctx(pktio_t *e)
+{
+	return e->ctx ? 0 : mi_cls_ctx_create(e->gpu, &e->ctx);
+}
+
+/* snapshot + upload when the control plane changed (caller: data path) */
+static int sync_rules(pktio_t *e, void *stream)
+{
+	if (e->compiled_gen == G.gen)
+		return 0;
+	pthread_mutex_lock(&G.lock);
+	uint64_t gen = G.gen;
+	long need = compile_locked(e, NULL, 0);
+
+	if (need < 0) {
+		pthread_mutex_unlock(&G.lock);
+		return (int)need;
+	}
+	if ((size_t)need > e->blob_cap) {
+		free(e->blob);
+		e->blob = malloc((size_t)need);
+		e->blob_cap = e->blob ? (size_t)need : 0;
+		if (!e->blob) {
+			pthread_mutex_unlock(&G.lock);
+			return -ENOMEM;
+		}
+	}
+	compile_locked(e, e->blob, e->blob_cap);
+	pthread_mutex_unlock(&G.lock);
+	int rc = mi_cls_rules_load(e->ctx, e->blob, (size_t)need, stream);
+
+	if (rc)
+		return rc;
+	int any = 0;
+
+	for (int i = 0; i < 8; i++)
+		any |= e->stats_mask[i] != 0;
+	mi_cls_stats_enable(e->ctx, any ? e->stats_mask : NULL);
+	e->compiled_gen = gen;
+	return 0;
+}
+
+/* Parse-only context: an empty table (no default / error CoS), so every
+ * record carries the parse result and outcome DISCARD / PARSE_DROP. */
+static int ensure_parse_ctx(pktio_t *e)
+{
+	if (e->pctx)
+		return 0;
+	int rc = mi_cls_ctx_create(e->gpu, &e->pctx);
+
+	if (rc)
+		return rc;
+	mi_tbl_hdr_t h;
+
+	memset(&h, 0, sizeof(h));
+	h.magic = MI_CLS_TBL_MAGIC;
+	h.version = MI_CLS_TBL_VERSION;
+	h.total_bytes = sizeof(h);
+	h.default_cos = -1;
+	h.error_cos = -1;
+	h.max_hops = 1;
+	h.cos_off = h.rule_off = h.term_off = sizeof(h);
+	rc = mi_cls_rules_load(e->pctx, &h, sizeof(h), NULL);
+	if (rc) {
+		mi_cls_ctx_destroy(e->pctx);
+		e->pctx = NULL;
+	}
+	return rc;
+}
+
+int odp_amd_cls_classify_host(odp_pktio_t h, const uint8_t *pkts, size_t bytes,
+			      const uint32_t *off, const uint16_t *len, uint32_t n, void *out,
+			      int parse_only)
+{
+	pktio_t *e = get_pktio(h);
+	int rc;
+
+	if (!e)
+		return -EINVAL;
+	if (parse_only) {
+		rc = ensure_parse_ctx(e);
+		if (rc)
+			return rc;
+		return mi_cls_classify_host(e->pctx, pkts, bytes, off, len, n,
+					    (mi_cls_result_t *)out);
+	}
+	rc = ensure_ctx(e);
+	if (rc)
+		return rc;
+	rc = sync_rules(e, NULL);
+	if (rc)
+		return rc;
+	return mi_cls_classify_host(e->ctx, pkts, bytes, off, len, n, (mi_cls_result_t *)out);
+}
+
+/* pktio start: device context, rule snapshot and a warm-up launch, so the
+ * first received burst does not pay for GPU initialisation. */
+int odp_amd_cls_prepare(odp_pktio_t h, int parse_only)
+{
+	static const uint8_t frame[64];
+	const uint32_t off = 0;
+	const uint16_t len = 60;
+	mi_cls_result_t r;
+
+	return odp_amd_cls_classify_host(h, frame, sizeof(frame), &off, &len, 1, &r, parse_only);
+}
+
+/* ---- odp_cls_hash_result (:407-437): the host form of get_dest_queue ---- */
+static const uint32_t rss_key[10] = {
+	0x6d5a56dau, 0x255b0ec2u, 0x4167253du, 0x43a38fb0u, 0xd0ca2bcbu,
+	0xae7b30b4u, 0x77cb2da3u, 0x8030f20cu, 0x6a42b73bu, 0xbeac01fau,
+};
+
+/* thash_softrss (protocols/thash.h:82-99), one tuple word */
+static uint32_t thash_word(uint32_t w, uint32_t j)
+{
+	uint32_t h = 0, i;
+
+	for (i = 0; i < 32; i++)
+		if (w & (1u << (31 - i)))
+			h ^= (rss_key[j] << i) | (i ? rss_key[j + 1] >> (32 - i) : 0u);
+	return h;
+}
+
+static uint32_t rd32(const uint8_t *p)
+{
+	uint32_t v;
+
+	memcpy(&v, p, 4);
+	return v;
+}
+
+/* packet_rss_hash (:1773-1839) over a parsed frame */
+uint32_t odp_amd_cls_rss_hash(const uint8_t *base, uint64_t in_flags, uint32_t l3, uint32_t l4,
+			      uint32_t hp)
+{
+	const uint64_t F_IPV4 = 1ull << 13, F_IPV6 = 1ull << 14, F_UDP = 1ull << 22,
+		       F_TCP = 1ull << 23;
+	uint32_t h = 0, j = 0, i;
+	int l4on = ((in_flags & F_TCP) && (hp & 8u)) || ((in_flags & F_UDP) && (hp & 4u));
+
+	if (in_flags & F_IPV4) {
+		if (hp & 1u) {
+			h ^= thash_word(rd32(base + l3 + 12), 0);
+			h ^= thash_word(rd32(base + l3 + 16), 1);
+			j = 2;
+		}
+		if (l4on && j == 2)   /* L4 without L3: undefined in the reference */
+			h ^= thash_word(rd32(base + l4), 2);
+	} else if (in_flags & F_IPV6) {
+		if (hp & 2u) {
+			for (i = 0; i < 4; i++) {
+				h ^= thash_word(__builtin_bswap32(rd32(base + l3 + 8 + 4 * i)), i);
+				h ^= thash_word(__builtin_bswap32(rd32(base + l3 + 24 + 4 * i)), 4 + i);
+			}
+			j = 8;
+		}
+		if (l4on && j == 8)
+			h ^= thash_word(rd32(base + l4), 8);
+	}
+	return h;
+}
+
+/* runtime accessor (odp_rt.c) */
+int _odp_amd_packet_parse_info(odp_packet_t pkt, const uint8_t **data, uint64_t *in_flags,
+			       uint32_t *l3, uint32_t *l4);
+
+odp_queue_t odp_cls_hash_result(odp_cos_t h, odp_packet_t packet)
+{
+	cos_t *c = get_cos(h);
+	const uint8_t *data;
+	uint64_t fl;
+	uint32_t l3, l4;
+
+	if (!c || packet == ODP_PACKET_INVALID)
+		return ODP_QUEUE_INVALID;
+	if (c->num_queue == 1)
+		return c->queue;
+	if (_odp_amd_packet_parse_info(packet, &data, &fl, &l3, &l4))
+		return ODP_QUEUE_INVALID;
+	uint32_t hash = odp_amd_cls_rss_hash(data, fl, l3, l4, c->hash_proto) & (COS_QUEUE_MAX - 1);
+
+	return c->hq[hash % c->num_queue];
 }

@@ -1,0 +1,1288 @@
+/*
+ * odp_pktio.c -- packet I/O for the MI355X build: the "loop" and "pcap"
+ * drivers and the GPU receive path they share.
+ *
+ * Reference behaviour:
+ *   platform/linux-generic/odp_packet_io.c  (open/config/start/stop/close,
+ *                                            pktin/pktout queue config)
+ *   platform/linux-generic/pktio/loop.c:253-384   loopback_recv
+ *   platform/linux-generic/pktio/pcap.c:90-401    devname parsing, promisc
+ *                                                 filter, pcapif_recv_pkt
+ *   include/odp_classification_internal.h:142-236 _odp_cls_enq run batching
+ *
+ * The receive path replaces the reference's per-packet
+ *   _odp_packet_parse_common() + _odp_cls_classify_packet()
+ * with ONE batched GPU launch per burst: the burst's frames are packed into a
+ * pinned staging buffer at 64-byte aligned offsets, parsed and classified by
+ * mi_cls_kernel (odp_amd_cls_classify_host -> mi_cls_classify_host), and the
+ * 16-byte result records drive the host side exactly as the reference's
+ * return codes do:
+ *   parse != 0            -> in_errors++        (loop.c:311-312)
+ *   parse  < 0            -> drop               (loop.c:314-317)
+ *   classify < 0          -> in_discards++, drop (loop.c:324-330)
+ *   classify > 0 (DROP)   -> drop
+ *   pool switch           -> copy into the CoS pool (loop.c:332-337)
+ *   no error flags        -> in_packets / in_octets (loop.c:352-355)
+ *   enqueue               -> runs of equal (dst_queue, cos) in arrival order
+ *                            (_odp_cls_enq / _odp_cos_enq + queue stats)
+ * The pcap reader (classic pcap and pcapng, both byte orders) replaces
+ * libpcap, which this image does not have.
+ */
+#define _GNU_SOURCE
+#include <errno.h>
+#include <inttypes.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/time.h>
+
+#include "odp_rt_internal.h"
+#include "mi_cls.h"
+
+enum { DRV_LOOP = 1, DRV_PCAP, DRV_NULL };
+enum { ST_OPENED = 0, ST_STARTED, ST_STOPPED };
+
+#define RX_BURST_DEFAULT 4096
+#define PCAP_MTU_MAX (64 * 1024)
+
+typedef struct {
+	int used;
+	char name[ODP_PKTIO_NAME_LEN];
+	int drv;
+	odp_pktio_t hdl;
+	odp_pool_t pool;
+	odp_pktio_param_t param;
+	odp_pktio_config_t config;
+	odp_pktin_queue_param_t inq_param;
+	odp_queue_t inq;            /* SCHED / QUEUE mode input queue */
+	int inq_configured;
+	uint32_t num_out;
+	int state;
+	int cls_enabled;
+	odp_proto_layer_t parse_layer;
+	int promisc;
+	odp_spinlock_t rxl;
+	odp_atomic_u64_t in_octets, in_packets, in_discards, in_errors;
+	odp_atomic_u64_t out_octets, out_packets, out_discards;
+	/* pcap */
+	uint8_t *fbuf;
+	uint32_t *foff;
+	uint16_t *flen;
+	uint32_t nframes, next;
+	int loops, loop_cnt, eof;
+	FILE *tx;
+	/* loop */
+	odp_queue_t loopq;
+	/* staging for the GPU burst */
+	uint8_t *stage;
+	int stage_pinned;
+	size_t stage_cap;
+	uint32_t *soff;
+	uint16_t *slen;
+	mi_cls_result_t *res;
+	odp_packet_t *pk;
+	uint32_t n_cap;
+} rt_pktio_t;
+
+static void stage_free(rt_pktio_t *e);
+
+static rt_pktio_t PK[RT_MAX_PKTIO];
+static odp_spinlock_t pk_lock;
+/* started SCHED-mode pktios, polled from odp_schedule*() */
+static int sched_list[RT_MAX_PKTIO];
+static int num_sched_pktio;
+
+static const uint8_t pcap_mac[6] = { 0x02, 0x00, 0x00, 0x00, 0x00, 0x02 };
+static const uint8_t loop_mac[6] = { 0x02, 0xe9, 0x34, 0x80, 0x73, 0x01 };
+
+uint32_t rt_gpu_index(void)
+{
+	const char *e = getenv("ODP_AMD_GPU");
+
+	return e ? (uint32_t)atoi(e) : 0u;
+}
+
+static uint32_t rx_burst(void)
+{
+	static uint32_t b;
+
+	if (!b) {
+		const char *e = getenv("ODP_AMD_RX_BURST");
+
+		b = e && atoi(e) > 0 ? (uint32_t)atoi(e) : RX_BURST_DEFAULT;
+	}
+	return b;
+}
+
+static rt_pktio_t *get_pk(odp_pktio_t h)
+{
+	uintptr_t i = (uintptr_t)h;
+
+	if (i == 0 || i > RT_MAX_PKTIO || !PK[i - 1].used)
+		return NULL;
+	return &PK[i - 1];
+}
+
+/* ============================================================ pcap reader */
+static uint32_t rd32s(const uint8_t *p, int swap)
+{
+	uint32_t v;
+
+	memcpy(&v, p, 4);
+	return swap ? __builtin_bswap32(v) : v;
+}
+
+static uint16_t rd16s(const uint8_t *p, int swap)
+{
+	uint16_t v;
+
+	memcpy(&v, p, 2);
+	return swap ? __builtin_bswap16(v) : v;
+}
+
+/* append one frame to the packed, 64 B aligned frame store */
+static int frame_add(rt_pktio_t *e, const uint8_t *d, uint32_t caplen, size_t *cap_b,
+		     uint32_t *cap_n, size_t *used_b)
+{
+	if (caplen > 65535 || caplen == 0)
+		return 0;   /* longer than the u16 descriptor: not received */
+	if (e->nframes == *cap_n) {
+		uint32_t nn = *cap_n ? *cap_n * 2 : 1024;
+		uint32_t *o = realloc(e->foff, nn * sizeof(uint32_t));
+		uint16_t *l = o ? realloc(e->flen, nn * sizeof(uint16_t)) : NULL;
+
+		if (!o || !l)
+			return -1;
+		e->foff = o;
+		e->flen = l;
+		*cap_n = nn;
+	}
+	size_t need = *used_b + ((caplen + 63u) & ~63u);
+
+	if (need > *cap_b) {
+		size_t nb = *cap_b ? *cap_b : (1u << 20);
+
+		while (nb < need)
+			nb *= 2;
+		uint8_t *b = realloc(e->fbuf, nb);
+
+		if (!b)
+			return -1;
+		memset(b + *cap_b, 0, nb - *cap_b);
+		e->fbuf = b;
+		*cap_b = nb;
+	}
+	memcpy(e->fbuf + *used_b, d, caplen);
+	e->foff[e->nframes] = (uint32_t)*used_b;
+	e->flen[e->nframes] = (uint16_t)caplen;
+	e->nframes++;
+	*used_b = need;
+	return 0;
+}
+
+/* Classic pcap (0xa1b2c3d4 / 0xa1b23c4d, either byte order) and pcapng
+ * (SHB / IDB / EPB / SPB / PB blocks).  Only DLT_EN10MB (1) is accepted,
+ * as in _pcapif_init_rx (pcap.c:130-134).  Returns 0 / -1. */
+static int pcap_load(rt_pktio_t *e, const char *fname)
+{
+	FILE *f = fopen(fname, "rb");
+	uint8_t *buf = NULL;
+	long sz;
+	size_t cap_b = 0, used_b = 0;
+	uint32_t cap_n = 0;
+	int rc = -1;
+
+	if (!f) {
+		RT_ERR("failed to open pcap file %s (%s)\n", fname, strerror(errno));
+		return -1;
+	}
+	if (fseek(f, 0, SEEK_END) || (sz = ftell(f)) < 0 || fseek(f, 0, SEEK_SET))
+		goto out;
+	buf = malloc((size_t)sz + 1);
+	if (!buf || fread(buf, 1, (size_t)sz, f) != (size_t)sz)
+		goto out;
+	if (sz < 24)
+		goto bad;
+	uint32_t m = rd32s(buf, 0);
+
+	if (m == 0xa1b2c3d4u || m == 0xa1b23c4du || m == 0xd4c3b2a1u || m == 0x4d3cb2a1u) {
+		int sw = (m == 0xd4c3b2a1u || m == 0x4d3cb2a1u);
+
+		if ((rd32s(buf + 20, sw) & 0x0fffffffu) != 1u) {
+			RT_ERR("unsupported datalink type: %u\n", rd32s(buf + 20, sw));
+			goto out;
+		}
+		for (long p = 24; p + 16 <= sz;) {
+			uint32_t incl = rd32s(buf + p + 8, sw);
+
+			if (p + 16 + (long)incl > sz)
+				break;
+			if (frame_add(e, buf + p + 16, incl, &cap_b, &cap_n, &used_b))
+				goto out;
+			p += 16 + incl;
+		}
+		rc = 0;
+	} else if (m == 0x0a0d0d0au) {
+		int sw = 0;
+		uint32_t link[64], nif = 0, snap[64];
+
+		for (long p = 0; p + 12 <= sz;) {
+			uint32_t type = rd32s(buf + p, sw);
+
+			if (type == 0x0a0d0d0au) {   /* section header: byte order */
+				uint32_t bom;
+
+				memcpy(&bom, buf + p + 8, 4);
+				sw = bom == 0x4d3c2b1au;
+				nif = 0;
+			}
+			uint32_t blen = rd32s(buf + p + 4, sw);
+
+			if (blen < 12 || p + (long)blen > sz)
+				break;
+			const uint8_t *b = buf + p + 8;
+
+			if (type == 1 && nif < 64) {             /* interface description */
+				link[nif] = rd16s(b, sw);
+				snap[nif] = rd32s(b + 4, sw);
+				nif++;
+			} else if (type == 6 && blen >= 32) {   /* enhanced packet */
+				uint32_t ifc = rd32s(b, sw), cap = rd32s(b + 12, sw);
+
+				if (ifc < nif && link[ifc] != 1)
+					goto bad_link;
+				if (20 + cap <= blen - 12 &&
+				    frame_add(e, b + 20, cap, &cap_b, &cap_n, &used_b))
+					goto out;
+			} else if (type == 3 && blen >= 16) {   /* simple packet */
+				uint32_t olen = rd32s(b, sw), cap = olen;
+
+				if (nif && link[0] != 1)
+					goto bad_link;
+				if (nif && snap[0] && cap > snap[0])
+					cap = snap[0];
+				if (4 + cap <= blen - 12 &&
+				    frame_add(e, b + 4, cap, &cap_b, &cap_n, &used_b))
+					goto out;
+			} else if (type == 2 && blen >= 32) {   /* obsolete packet block */
+				uint32_t ifc = rd16s(b, sw), cap = rd32s(b + 12, sw);
+
+				if (ifc < nif && link[ifc] != 1)
+					goto bad_link;
+				if (20 + cap <= blen - 12 &&
+				    frame_add(e, b + 20, cap, &cap_b, &cap_n, &used_b))
+					goto out;
+			}
+			p += blen;
+		}
+		rc = 0;
+	} else {
+		goto bad;
+	}
+	goto out;
+bad_link:
+	RT_ERR("unsupported datalink type in %s\n", fname);
+	goto out;
+bad:
+	RT_ERR("%s: not a pcap / pcapng file\n", fname);
+out:
+	free(buf);
+	fclose(f);
+	return rc;
+}
+
+static int pcap_dump_open(rt_pktio_t *e, const char *fname)
+{
+	const uint32_t hdr[6] = { 0xa1b2c3d4u, 0x00040002u, 0, 0, PCAP_MTU_MAX, 1 };
+
+	e->tx = fopen(fname, "wb");
+	if (!e->tx) {
+		RT_ERR("failed to open dump file %s\n", fname);
+		return -1;
+	}
+	fwrite(hdr, sizeof(hdr), 1, e->tx);
+	fflush(e->tx);
+	return 0;
+}
+
+static void pcap_dump(rt_pktio_t *e, odp_packet_t pkt)
+{
+	struct timeval tv;
+	uint32_t h[4];
+	pkt_hdr_t *p = rt_pkt_hdr(pkt);
+
+	gettimeofday(&tv, NULL);
+	h[0] = (uint32_t)tv.tv_sec;
+	h[1] = (uint32_t)tv.tv_usec;
+	h[2] = h[3] = p->len;
+	fwrite(h, sizeof(h), 1, e->tx);
+	fwrite(p->head + p->data_off, 1, p->len, e->tx);
+	fflush(e->tx);
+}
+
+/* _pcapif_parse_devname (pcap.c:90-117) */
+static int pcap_open(rt_pktio_t *e, const char *devname)
+{
+	char in[ODP_PKTIO_NAME_LEN], *tok, *save = NULL;
+	char *rx = NULL, *txn = NULL;
+	int rc = 0;
+
+	snprintf(in, sizeof(in), "%s", devname);
+	e->loops = 1;
+	e->loop_cnt = 1;
+	for (tok = strtok_r(in + 5, ":", &save); tok; tok = strtok_r(NULL, ":", &save)) {
+		if (strncmp(tok, "in=", 3) == 0 && !rx) {
+			rx = strdup(tok + 3);
+		} else if (strncmp(tok, "out=", 4) == 0 && !txn) {
+			txn = strdup(tok + 4);
+		} else if (strncmp(tok, "loops=", 6) == 0) {
+			e->loops = atoi(tok + 6);
+			if (e->loops < 0) {
+				RT_ERR("invalid loop count\n");
+				rc = -1;
+			}
+		}
+	}
+	if (!rc && rx)
+		rc = pcap_load(e, rx);
+	if (!rc && txn)
+		rc = pcap_dump_open(e, txn);
+	if (!rc && !rx && !txn)
+		rc = -1;
+	free(rx);
+	free(txn);
+	e->promisc = 0;   /* pcapif_init sets promisc off (pcap.c:232) */
+	return rc;
+}
+
+/* BPF "ether dst <pcap_mac> or broadcast or multicast" (pcap.c:176-186) */
+static int pcap_filter_pass(const rt_pktio_t *e, const uint8_t *d, uint32_t len)
+{
+	if (e->promisc)
+		return 1;
+	if (len < 6)
+		return 0;
+	return memcmp(d, pcap_mac, 6) == 0 || (d[0] & 1u);
+}
+
+/* ============================================================ open / config */
+void odp_pktio_param_init(odp_pktio_param_t *p)
+{
+	memset(p, 0, sizeof(*p));
+	p->in_mode = ODP_PKTIN_MODE_DIRECT;
+	p->out_mode = ODP_PKTOUT_MODE_DIRECT;
+}
+
+void odp_pktin_queue_param_init(odp_pktin_queue_param_t *p)
+{
+	memset(p, 0, sizeof(*p));
+	p->op_mode = ODP_PKTIO_OP_MT;
+	p->num_queues = 1;
+	p->classifier_enable = 0;
+	odp_queue_param_init(&p->queue_param);
+	p->queue_param.type = ODP_QUEUE_TYPE_SCHED;
+}
+
+void odp_pktout_queue_param_init(odp_pktout_queue_param_t *p)
+{
+	memset(p, 0, sizeof(*p));
+	p->op_mode = ODP_PKTIO_OP_MT;
+	p->num_queues = 1;
+}
+
+void odp_pktio_config_init(odp_pktio_config_t *c)
+{
+	memset(c, 0, sizeof(*c));
+	c->parser.layer = ODP_PROTO_LAYER_ALL;
+	c->reassembly.max_num_frags = 2;
+}
+
+odp_pktio_t odp_pktio_open(const char *name, odp_pool_t pool, const odp_pktio_param_t *param)
+{
+	odp_pktio_param_t def;
+	int drv;
+
+	if (!name)
+		return ODP_PKTIO_INVALID;
+	if (strncmp(name, "pcap:", 5) == 0)
+		drv = DRV_PCAP;
+	else if (strncmp(name, "loop", 4) == 0)
+		drv = DRV_LOOP;
+	else if (strncmp(name, "null", 4) == 0)
+		drv = DRV_NULL;
+	else {
+		RT_ERR("pktio %s: no driver (this build has loop, pcap:in=/out=, null)\n", name);
+		return ODP_PKTIO_INVALID;
+	}
+	rt_pool_t *pp = rt_pool(pool);
+
+	if (!pp || pp->param.type != ODP_POOL_PACKET) {
+		RT_ERR("pktio %s: invalid packet pool\n", name);
+		return ODP_PKTIO_INVALID;
+	}
+	if (!param) {
+		odp_pktio_param_init(&def);
+		param = &def;
+	}
+	if (odp_pktio_lookup(name) != ODP_PKTIO_INVALID) {
+		RT_ERR("pktio %s already open\n", name);
+		return ODP_PKTIO_INVALID;
+	}
+	/* the classifier endpoint (classifier_t + device context) gives the handle */
+	odp_pktio_t h = odp_amd_cls_pktio_create((int)rt_gpu_index());
+
+	if (h == ODP_PKTIO_INVALID)
+		return h;
+	rt_pktio_t *e = &PK[(uintptr_t)h - 1];
+
+	odp_spinlock_lock(&pk_lock);
+	memset(e, 0, sizeof(*e));
+	e->used = 1;
+	odp_spinlock_unlock(&pk_lock);
+	snprintf(e->name, sizeof(e->name), "%s", name);
+	e->drv = drv;
+	e->hdl = h;
+	e->pool = pool;
+	e->param = *param;
+	odp_pktio_config_init(&e->config);
+	odp_spinlock_init(&e->rxl);
+	e->state = ST_OPENED;
+	e->promisc = 1;
+	if (drv == DRV_PCAP && pcap_open(e, name)) {
+		free(e->fbuf);
+		free(e->foff);
+		free(e->flen);
+		e->used = 0;
+		odp_amd_cls_pktio_destroy(h);
+		return ODP_PKTIO_INVALID;
+	}
+	if (drv == DRV_LOOP) {
+		odp_queue_param_t qp;
+		char qn[ODP_QUEUE_NAME_LEN];
+
+		odp_queue_param_init(&qp);
+		snprintf(qn, sizeof(qn), "%.20s_loopq", name);
+		e->loopq = odp_queue_create(qn, &qp);
+		if (e->loopq == ODP_QUEUE_INVALID) {
+			e->used = 0;
+			odp_amd_cls_pktio_destroy(h);
+			return ODP_PKTIO_INVALID;
+		}
+	}
+	/* default queue config as odp_pktio_open does for DISABLED-less modes */
+	odp_pktin_queue_param_init(&e->inq_param);
+	return h;
+}
+
+odp_pktio_t odp_pktio_lookup(const char *name)
+{
+	for (int i = 0; i < RT_MAX_PKTIO; i++)
+		if (PK[i].used && name && strcmp(PK[i].name, name) == 0)
+			return PK[i].hdl;
+	return ODP_PKTIO_INVALID;
+}
+
+int odp_pktio_capability(odp_pktio_t h, odp_pktio_capability_t *c)
+{
+	rt_pktio_t *e = get_pk(h);
+
+	if (!e || !c)
+		return -1;
+	memset(c, 0, sizeof(*c));
+	c->max_input_queues = 1;
+	c->max_output_queues = e->drv == DRV_LOOP ? ODP_PKTOUT_MAX_QUEUES : 1;
+	c->max_input_queue_size = 0;
+	c->max_output_queue_size = 0;
+	odp_pktio_config_init(&c->config);
+	c->config.parser.layer = ODP_PROTO_LAYER_ALL;
+	c->config.enable_loop = 0;
+	c->set_op.op.promisc_mode = e->drv == DRV_PCAP;
+	c->maxlen.equal = 1;
+	c->maxlen.min_input = c->maxlen.min_output = 68 + 14;
+	c->maxlen.max_input = c->maxlen.max_output = 65535;
+	c->loop_supported = ODP_SUPPORT_NO;
+	return 0;
+}
+
+int odp_pktio_config(odp_pktio_t h, const odp_pktio_config_t *config)
+{
+	rt_pktio_t *e = get_pk(h);
+	odp_pktio_config_t def;
+
+	if (!e)
+		return -1;
+	if (!config) {
+		odp_pktio_config_init(&def);
+		config = &def;
+	}
+	/* only parser options and the zero checksum/ts options are supported */
+	if (config->pktin.all_bits || config->pktout.all_bits || config->enable_loop ||
+	    config->inbound_ipsec || config->outbound_ipsec || config->enable_lso) {
+		RT_ERR("pktio %s: unsupported configuration option\n", e->name);
+		return -1;
+	}
+	if (e->state == ST_STARTED)
+		return -1;
+	e->config = *config;
+	return 0;
+}
+
+int odp_pktin_queue_config(odp_pktio_t h, const odp_pktin_queue_param_t *param)
+{
+	rt_pktio_t *e = get_pk(h);
+	odp_pktin_queue_param_t def;
+
+	if (!e || e->state == ST_STARTED)
+		return -1;
+	if (!param) {
+		odp_pktin_queue_param_init(&def);
+		param = &def;
+	}
+	if (e->param.in_mode == ODP_PKTIN_MODE_DISABLED)
+		return -1;
+	if (param->num_queues > 1 || (param->num_queues == 0 && !param->classifier_enable)) {
+		RT_ERR("pktio %s: %u input queues requested, 1 supported\n", e->name,
+		       param->num_queues);
+		return -1;
+	}
+	if (param->vector.enable) {
+		RT_ERR("pktio %s: packet vectors are not supported\n", e->name);
+		return -1;
+	}
+	if (e->inq != ODP_QUEUE_INVALID) {
+		odp_queue_destroy(e->inq);
+		e->inq = ODP_QUEUE_INVALID;
+	}
+	e->inq_param = *param;
+	e->cls_enabled = param->classifier_enable;
+	if (e->param.in_mode == ODP_PKTIN_MODE_SCHED || e->param.in_mode == ODP_PKTIN_MODE_QUEUE) {
+		odp_queue_param_t qp = param->queue_param;
+		char qn[ODP_QUEUE_NAME_LEN];
+
+		qp.type = e->param.in_mode == ODP_PKTIN_MODE_SCHED ? ODP_QUEUE_TYPE_SCHED
+								    : ODP_QUEUE_TYPE_PLAIN;
+		snprintf(qn, sizeof(qn), "odp-pktin-%d-0", (int)((uintptr_t)h - 1));
+		e->inq = odp_queue_create(qn, &qp);
+		if (e->inq == ODP_QUEUE_INVALID)
+			return -1;
+		if (e->param.in_mode == ODP_PKTIN_MODE_QUEUE)
+			((rt_queue_t *)(void *)e->inq)->pktin_idx = (int)(uintptr_t)h;
+	}
+	e->inq_configured = 1;
+	return 0;
+}
+
+int odp_pktout_queue_config(odp_pktio_t h, const odp_pktout_queue_param_t *param)
+{
+	rt_pktio_t *e = get_pk(h);
+	odp_pktio_capability_t c;
+
+	if (!e || e->state == ST_STARTED || odp_pktio_capability(h, &c))
+		return -1;
+	uint32_t n = param ? param->num_queues : 1;
+
+	if (n == 0 || n > c.max_output_queues)
+		return -1;
+	e->num_out = n;
+	return 0;
+}
+
+int odp_pktin_queue(odp_pktio_t h, odp_pktin_queue_t q[], int num)
+{
+	rt_pktio_t *e = get_pk(h);
+
+	if (!e || e->param.in_mode != ODP_PKTIN_MODE_DIRECT)
+		return -1;
+	if (num > 0 && q) {
+		q[0].q = (_odp_pktin_hdl_t)(uintptr_t)h;
+		q[0].index = 0;
+		q[0].pktio = h;
+	}
+	return 1;
+}
+
+int odp_pktin_event_queue(odp_pktio_t h, odp_queue_t q[], int num)
+{
+	rt_pktio_t *e = get_pk(h);
+
+	if (!e || (e->param.in_mode != ODP_PKTIN_MODE_SCHED &&
+		   e->param.in_mode != ODP_PKTIN_MODE_QUEUE))
+		return -1;
+	if (num > 0 && q)
+		q[0] = e->inq;
+	return e->inq != ODP_QUEUE_INVALID ? 1 : 0;
+}
+
+int odp_pktout_queue(odp_pktio_t h, odp_pktout_queue_t q[], int num)
+{
+	rt_pktio_t *e = get_pk(h);
+
+	if (!e || e->param.out_mode != ODP_PKTOUT_MODE_DIRECT)
+		return -1;
+	if (!e->num_out)
+		e->num_out = 1;
+	for (int i = 0; i < num && (uint32_t)i < e->num_out; i++) {
+		q[i].q = (void *)(uintptr_t)h;
+		q[i].index = i;
+		q[i].pktio = h;
+	}
+	return (int)e->num_out;
+}
+
+int odp_pktio_start(odp_pktio_t h)
+{
+	rt_pktio_t *e = get_pk(h);
+
+	if (!e)
+		return -1;
+	if (e->state == ST_STARTED) {
+		RT_ERR("Already started\n");
+		return -1;
+	}
+	if (!e->inq_configured && e->param.in_mode != ODP_PKTIN_MODE_DISABLED &&
+	    odp_pktin_queue_config(h, NULL))
+		return -1;
+	/* odp_packet_io.c:675-677 */
+	e->parse_layer = e->cls_enabled ? ODP_PROTO_LAYER_ALL : e->config.parser.layer;
+	/* GPU context, rule snapshot and a warm-up launch before traffic */
+	if (e->param.in_mode != ODP_PKTIN_MODE_DISABLED && e->parse_layer != ODP_PROTO_LAYER_NONE) {
+		int rc = odp_amd_cls_prepare(h, !e->cls_enabled);
+
+		if (rc) {
+			RT_ERR("pktio %s: GPU receive path unavailable (%s)\n", e->name,
+			       mi_cls_strerror(rc));
+			return -1;
+		}
+	}
+	e->state = ST_STARTED;
+	if (e->param.in_mode == ODP_PKTIN_MODE_SCHED) {
+		odp_spinlock_lock(&pk_lock);
+		sched_list[num_sched_pktio++] = (int)((uintptr_t)h - 1);
+		odp_spinlock_unlock(&pk_lock);
+	}
+	return 0;
+}
+
+static void sched_list_remove(int idx)
+{
+	odp_spinlock_lock(&pk_lock);
+	for (int i = 0; i < num_sched_pktio; i++)
+		if (sched_list[i] == idx) {
+			sched_list[i] = sched_list[--num_sched_pktio];
+			break;
+		}
+	odp_spinlock_unlock(&pk_lock);
+}
+
+int odp_pktio_stop(odp_pktio_t h)
+{
+	rt_pktio_t *e = get_pk(h);
+
+	if (!e || e->state != ST_STARTED) {
+		RT_ERR("Not started\n");
+		return -1;
+	}
+	sched_list_remove((int)((uintptr_t)h - 1));
+	odp_spinlock_lock(&e->rxl);   /* wait for an in-flight burst */
+	e->state = ST_STOPPED;
+	odp_spinlock_unlock(&e->rxl);
+	return 0;
+}
+
+int odp_pktio_close(odp_pktio_t h)
+{
+	rt_pktio_t *e = get_pk(h);
+
+	if (!e)
+		return -1;
+	if (e->state == ST_STARTED) {
+		RT_ERR("pktio %s: close while started\n", e->name);
+		return -1;
+	}
+	if (e->inq != ODP_QUEUE_INVALID) {
+		odp_event_t ev[64];
+		int n;
+
+		while ((n = rt_queue_deq_multi_raw((rt_queue_t *)(void *)e->inq, ev, 64)) > 0)
+			odp_event_free_multi(ev, n);
+		odp_queue_destroy(e->inq);
+	}
+	if (e->loopq != ODP_QUEUE_INVALID) {
+		odp_event_t ev[64];
+		int n;
+
+		while ((n = rt_queue_deq_multi_raw((rt_queue_t *)(void *)e->loopq, ev, 64)) > 0)
+			odp_event_free_multi(ev, n);
+		odp_queue_destroy(e->loopq);
+	}
+	if (e->tx)
+		fclose(e->tx);
+	free(e->fbuf);
+	free(e->foff);
+	free(e->flen);
+	stage_free(e);
+	free(e->soff);
+	free(e->slen);
+	free(e->res);
+	free(e->pk);
+	odp_spinlock_lock(&pk_lock);
+	memset(e, 0, sizeof(*e));
+	odp_spinlock_unlock(&pk_lock);
+	return odp_amd_cls_pktio_destroy(h);
+}
+
+/* ============================================================ receive */
+static void stage_free(rt_pktio_t *e)
+{
+	if (e->stage_pinned)
+		mi_cls_host_free(e->stage);
+	else
+		free(e->stage);
+	e->stage = NULL;
+}
+
+/* descriptor arrays for n frames; stage bytes grow keeping the contents */
+static int stage_reserve(rt_pktio_t *e, uint32_t n, size_t bytes)
+{
+	if (n > e->n_cap) {
+		uint32_t c = n < 256 ? 256 : n;
+
+		free(e->soff);
+		free(e->slen);
+		free(e->res);
+		free(e->pk);
+		e->soff = malloc(c * sizeof(uint32_t));
+		e->slen = malloc(c * sizeof(uint16_t));
+		e->res = malloc(c * sizeof(mi_cls_result_t));
+		e->pk = malloc(c * sizeof(odp_packet_t));
+		if (!e->soff || !e->slen || !e->res || !e->pk) {
+			e->n_cap = 0;
+			return -1;
+		}
+		e->n_cap = c;
+	}
+	if (bytes > e->stage_cap) {
+		size_t c = e->stage_cap ? e->stage_cap : (4u << 20);
+
+		while (c < bytes)
+			c *= 2;
+		/* pinned memory takes the DMA-direct H2D path; without a GPU
+		 * (parse layer NONE) pageable memory serves */
+		int pinned = 1;
+		uint8_t *ns = mi_cls_host_alloc(c);
+
+		if (!ns) {
+			ns = malloc(c);
+			pinned = 0;
+		}
+		if (!ns)
+			return -1;
+		if (e->stage) {
+			memcpy(ns, e->stage, e->stage_cap);
+			stage_free(e);
+		}
+		e->stage = ns;
+		e->stage_pinned = pinned;
+		e->stage_cap = c;
+	}
+	return 0;
+}
+
+/* Host-side masking for parser layers below L4 (odp_parse.c:372-414): the
+ * L2 / L3 parts of the full parse are identical at any layer; the layer only
+ * cuts what is recorded and whether an L4 truncation drops. */
+static void apply_layer(mi_cls_result_t *r, odp_proto_layer_t layer)
+{
+	/* l2 l3 eth eth_bcast eth_mcast jumbo vlan vlan_qinq */
+	const uint32_t L2F = (1u << 3) | (0x3fu << 6);
+	/* + l3 arp ipv4 ipv6 ip_bcast ip_mcast ipfrag ipopt */
+	const uint32_t L3F = L2F | (1u << 4) | (0x7fu << 12);
+
+	if (layer >= ODP_PROTO_LAYER_L4)
+		return;
+	if (r->outcome == MI_CLS_OUT_PARSE_DROP)
+		r->outcome = MI_CLS_OUT_DISCARD;
+	if (layer == ODP_PROTO_LAYER_L2) {
+		r->in_flags &= L2F;
+		r->err &= 0x01;     /* snap_len_err */
+		r->l4_offset = ODP_PACKET_OFFSET_INVALID;
+	} else {
+		r->in_flags &= L3F;
+		r->err &= 0x03;     /* snap_len_err, ip_err */
+	}
+}
+
+/* Enqueue a run of classified packets (_odp_cos_enq,
+ * odp_classification_internal.h:171-201) */
+static void cos_enq_run(odp_packet_t pk[], int num)
+{
+	pkt_hdr_t *h = rt_pkt_hdr(pk[0]);
+	int r = odp_queue_enq_multi(h->dst_queue, (const odp_event_t *)(void *)pk, num);
+
+	if (r < 0)
+		r = 0;
+	if (r != num)
+		odp_packet_free_multi(&pk[r], num - r);
+	/* the queue slot is recovered from the CoS's queue table */
+	uint32_t slot = 0;
+	odp_cos_t cos = (odp_cos_t)(uintptr_t)(h->cos + 1u);
+	uint32_t nq = odp_cls_cos_num_queue(cos);
+
+	if (nq > 1) {
+		odp_queue_t qs[32];
+
+		odp_cls_cos_queues(cos, qs, 32);
+		for (uint32_t i = 0; i < nq; i++)
+			if (qs[i] == h->dst_queue)
+				slot = i;
+	}
+	odp_amd_cls_queue_stats_add(h->cos, slot, (uint64_t)r, (uint64_t)(num - r));
+}
+
+/* Pull up to `max` frames from the driver into the staging buffer (64 B
+ * aligned offsets).  Loop frames keep their packets in e->pk; pcap frames are
+ * allocated later, directly from the final pool.  Returns the frame count. */
+static int stage_frames(rt_pktio_t *e, uint32_t max, size_t *bytes)
+{
+	uint32_t n = 0;
+	size_t off = 0;
+
+	if (stage_reserve(e, max, 0))
+		return -1;
+	if (e->drv == DRV_PCAP) {
+		while (n < max) {
+			if (e->next >= e->nframes) {
+				if (e->nframes == 0 || e->eof)
+					break;
+				/* _pcapif_reopen (pcap.c:257-278): note loop_cnt starts at 1 */
+				if (e->loops != 0 && ++e->loop_cnt >= e->loops) {
+					e->eof = 1;
+					break;
+				}
+				e->next = 0;
+			}
+			const uint8_t *d = e->fbuf + e->foff[e->next];
+			uint16_t l = e->flen[e->next];
+
+			e->next++;
+			if (!pcap_filter_pass(e, d, l))
+				continue;
+			if (stage_reserve(e, max, off + l + 64))
+				return -1;
+			memcpy(e->stage + off, d, l);
+			e->soff[n] = (uint32_t)off;
+			e->slen[n] = l;
+			off += ((uint32_t)l + 63u) & ~63u;
+			n++;
+		}
+	} else if (e->drv == DRV_LOOP) {
+		odp_event_t ev[256];
+
+		while (n < max) {
+			int want = max - n < 256 ? (int)(max - n) : 256;
+			int got = rt_queue_deq_multi_raw((rt_queue_t *)(void *)e->loopq, ev, want);
+
+			if (got <= 0)
+				break;
+			for (int i = 0; i < got; i++) {
+				odp_packet_t p = odp_packet_from_event(ev[i]);
+				pkt_hdr_t *h = rt_pkt_hdr(p);
+				uint32_t l = h->len > 65535 ? 65535 : h->len;
+
+				if (stage_reserve(e, max, off + l + 64)) {
+					odp_event_free_multi(&ev[i], got - i);
+					odp_packet_free_multi(e->pk, (int)n);
+					return -1;
+				}
+				memcpy(e->stage + off, h->head + h->data_off, l);
+				e->soff[n] = (uint32_t)off;
+				e->slen[n] = (uint16_t)l;
+				e->pk[n] = p;
+				off += (l + 63u) & ~63u;
+				n++;
+			}
+			if (got < want)
+				break;
+		}
+	}
+	*bytes = off + 64;
+	return (int)n;
+}
+
+/* One receive burst.  Unclassified packets are returned in out[] (at most
+ * max_out); classified ones are enqueued to their CoS queues. */
+static int pktio_recv(rt_pktio_t *e, odp_packet_t out[], int max_out)
+{
+	size_t bytes = 0;
+	uint32_t burst = rx_burst();
+
+	if (!e->cls_enabled && (uint32_t)max_out < burst)
+		burst = (uint32_t)max_out;
+	int n = stage_frames(e, burst, &bytes);
+
+	if (n <= 0)
+		return n;
+	const odp_proto_layer_t layer = e->parse_layer;
+
+	if (layer != ODP_PROTO_LAYER_NONE) {
+		int rc = odp_amd_cls_classify_host(e->hdl, e->stage, bytes, e->soff, e->slen,
+						   (uint32_t)n, e->res, !e->cls_enabled);
+
+		if (rc) {
+			RT_ERR("pktio %s: GPU classify failed (%s), burst of %d dropped\n", e->name,
+			       mi_cls_strerror(rc), n);
+			if (e->drv == DRV_LOOP)
+				odp_packet_free_multi(e->pk, n);
+			odp_atomic_add_u64(&e->in_discards, (uint64_t)n);
+			return 0;
+		}
+	}
+	odp_packet_t *run = e->pk;   /* reused in place: run[j] <= pk[i], j <= i */
+	int nrun = 0, num_rx = 0;
+	uint64_t octets = 0, packets = 0;
+
+	for (int i = 0; i < n; i++) {
+		mi_cls_result_t r;
+		odp_packet_t pkt = e->drv == DRV_LOOP ? e->pk[i] : ODP_PACKET_INVALID;
+		uint32_t len = e->slen[i];
+
+		if (layer != ODP_PROTO_LAYER_NONE) {
+			r = e->res[i];
+			apply_layer(&r, layer);
+			if (r.err || r.outcome == MI_CLS_OUT_PARSE_DROP)
+				odp_atomic_inc_u64(&e->in_errors);
+			if (r.outcome == MI_CLS_OUT_PARSE_DROP) {
+				odp_packet_free(pkt);
+				continue;
+			}
+		} else {
+			memset(&r, 0, sizeof(r));
+			r.cos = 0xff;
+		}
+		odp_pool_t pool = e->pool;
+
+		if (e->cls_enabled) {
+			if (r.outcome == MI_CLS_OUT_DISCARD || r.outcome == MI_CLS_OUT_LOOP)
+				odp_atomic_inc_u64(&e->in_discards);
+			if (r.outcome != MI_CLS_OUT_ENQ) {
+				odp_packet_free(pkt);
+				continue;
+			}
+			odp_pool_t cp = odp_amd_cls_pool_of(r.cos);
+
+			if (cp != ODP_POOL_INVALID)
+				pool = cp;
+		}
+		/* packet in the final pool (_odp_pktio_packet_to_pool) */
+		if (pkt == ODP_PACKET_INVALID) {
+			pkt = odp_packet_alloc(pool, len);
+			if (pkt == ODP_PACKET_INVALID) {
+				if (e->cls_enabled)
+					odp_atomic_inc_u64(&e->in_discards);
+				continue;
+			}
+			memcpy(odp_packet_data(pkt), e->stage + e->soff[i], len);
+		} else if (odp_packet_pool(pkt) != pool) {
+			odp_packet_t np = odp_packet_alloc(pool, len);
+
+			if (np == ODP_PACKET_INVALID) {
+				odp_packet_free(pkt);
+				odp_atomic_inc_u64(&e->in_discards);
+				continue;
+			}
+			pkt_hdr_t *sh = rt_pkt_hdr(pkt);
+
+			memcpy(odp_packet_data(np), sh->head + sh->data_off, len);
+			rt_pkt_hdr(np)->user_ptr = sh->user_ptr;
+			odp_packet_free(pkt);
+			pkt = np;
+		}
+		pkt_hdr_t *h = rt_pkt_hdr(pkt);
+
+		if (layer != ODP_PROTO_LAYER_NONE) {
+			h->in_flags = r.in_flags;
+			h->err = r.err;
+			h->l2 = 0;
+			h->l3 = r.l3_offset;
+			h->l4 = r.l4_offset;
+		} else {
+			h->in_flags = 0;
+			h->err = 0;
+		}
+		h->input = e->hdl;
+		if (!h->err) {
+			octets += len;
+			packets++;
+		}
+		if (e->cls_enabled) {
+			h->cos = r.cos;
+			h->cls_mark = r.mark;
+			h->dst_queue = odp_amd_cls_queue_of(r.cos, r.queue);
+			/* _odp_cls_enq: flush when (dst_queue, cos) changes */
+			if (nrun) {
+				pkt_hdr_t *ph = rt_pkt_hdr(run[nrun - 1]);
+
+				if (ph->dst_queue != h->dst_queue || ph->cos != h->cos) {
+					cos_enq_run(run, nrun);
+					nrun = 0;
+				}
+			}
+			run[nrun++] = pkt;
+		} else if (num_rx < max_out) {
+			out[num_rx++] = pkt;
+		} else {
+			odp_packet_free(pkt);
+		}
+	}
+	if (nrun)
+		cos_enq_run(run, nrun);
+	odp_atomic_add_u64(&e->in_octets, octets);
+	odp_atomic_add_u64(&e->in_packets, packets);
+	return num_rx;
+}
+
+/* receive into the pktin queue (SCHED / QUEUE modes) */
+static int poll_into_inq(rt_pktio_t *e)
+{
+	odp_packet_t pk[RX_BURST_DEFAULT];
+	int n;
+
+	if (!odp_spinlock_trylock(&e->rxl))
+		return 0;
+	if (e->state != ST_STARTED) {
+		odp_spinlock_unlock(&e->rxl);
+		return 0;
+	}
+	n = pktio_recv(e, pk, RX_BURST_DEFAULT);
+	odp_spinlock_unlock(&e->rxl);
+	if (n > 0) {
+		int r = odp_queue_enq_multi(e->inq, (const odp_event_t *)(void *)pk, n);
+
+		if (r < 0)
+			r = 0;
+		if (r < n) {
+			odp_packet_free_multi(&pk[r], n - r);
+			odp_atomic_add_u64(&e->in_discards, (uint64_t)(n - r));
+		}
+	}
+	return n;
+}
+
+int rt_pktio_sched_poll(void)
+{
+	int idx[RT_MAX_PKTIO], n, total = 0;
+
+	if (!__atomic_load_n(&num_sched_pktio, __ATOMIC_RELAXED))
+		return 0;
+	odp_spinlock_lock(&pk_lock);
+	n = num_sched_pktio;
+	memcpy(idx, sched_list, (size_t)n * sizeof(int));
+	odp_spinlock_unlock(&pk_lock);
+	for (int i = 0; i < n; i++)
+		total += poll_into_inq(&PK[idx[i]]);
+	return total;
+}
+
+int rt_pktio_poll_index(int idx)
+{
+	if (idx < 0 || idx >= RT_MAX_PKTIO || !PK[idx].used)
+		return 0;
+	return poll_into_inq(&PK[idx]);
+}
+
+int odp_pktin_recv(odp_pktin_queue_t q, odp_packet_t pkts[], int num)
+{
+	rt_pktio_t *e = get_pk(q.pktio);
+	int n;
+
+	if (!e || num < 0)
+		return -1;
+	if (e->state != ST_STARTED)
+		return 0;
+	odp_spinlock_lock(&e->rxl);
+	n = e->state == ST_STARTED ? pktio_recv(e, pkts, num) : 0;
+	odp_spinlock_unlock(&e->rxl);
+	return n;
+}
+
+uint64_t odp_pktin_wait_time(uint64_t nsec)
+{
+	return nsec;
+}
+
+int odp_pktin_recv_tmo(odp_pktin_queue_t q, odp_packet_t pkts[], int num, uint64_t wait)
+{
+	odp_time_t t0 = odp_time_local();
+
+	for (;;) {
+		int n = odp_pktin_recv(q, pkts, num);
+
+		if (n != 0 || wait == ODP_PKTIN_NO_WAIT)
+			return n;
+		if (wait != ODP_PKTIN_WAIT &&
+		    odp_time_diff_ns(odp_time_local(), t0) >= wait)
+			return 0;
+		odp_time_wait_ns(10 * ODP_TIME_USEC_IN_NS);
+	}
+}
+
+/* ============================================================ transmit */
+int odp_pktout_send(odp_pktout_queue_t q, const odp_packet_t pkts[], int num)
+{
+	rt_pktio_t *e = get_pk(q.pktio);
+
+	if (!e || num < 0)
+		return -1;
+	if (e->state != ST_STARTED)
+		return -1;
+	uint64_t octets = 0;
+
+	for (int i = 0; i < num; i++)
+		octets += odp_packet_len(pkts[i]);
+	if (e->drv == DRV_LOOP) {
+		int r = odp_queue_enq_multi(e->loopq, (const odp_event_t *)(const void *)pkts, num);
+
+		if (r < 0)
+			return -1;
+		odp_atomic_add_u64(&e->out_packets, (uint64_t)r);
+		odp_atomic_add_u64(&e->out_octets, octets);
+		return r;
+	}
+	for (int i = 0; i < num; i++) {
+		if (e->tx)
+			pcap_dump(e, pkts[i]);
+		odp_packet_free(pkts[i]);
+	}
+	odp_atomic_add_u64(&e->out_packets, (uint64_t)num);
+	odp_atomic_add_u64(&e->out_octets, octets);
+	return num;
+}
+
+/* ============================================================ misc */
+int odp_pktio_promisc_mode(odp_pktio_t h)
+{
+	rt_pktio_t *e = get_pk(h);
+
+	if (!e)
+		return -1;
+	return e->drv == DRV_PCAP ? e->promisc : 1;
+}
+
+int odp_pktio_promisc_mode_set(odp_pktio_t h, odp_bool_t enable)
+{
+	rt_pktio_t *e = get_pk(h);
+
+	if (!e || e->drv != DRV_PCAP || e->state == ST_STARTED)
+		return -1;
+	e->promisc = enable;
+	return 0;
+}
+
+int odp_pktio_mac_addr(odp_pktio_t h, void *mac, int size)
+{
+	rt_pktio_t *e = get_pk(h);
+
+	if (!e || size < 6)
+		return -1;
+	memcpy(mac, e->drv == DRV_PCAP ? pcap_mac : loop_mac, 6);
+	return 6;
+}
+
+uint32_t odp_pktio_mtu(odp_pktio_t h)
+{
+	rt_pktio_t *e = get_pk(h);
+
+	return e ? (e->drv == DRV_PCAP ? PCAP_MTU_MAX : 9216) : 0;
+}
+
+int odp_pktio_stats(odp_pktio_t h, odp_pktio_stats_t *s)
+{
+	rt_pktio_t *e = get_pk(h);
+
+	if (!e || !s)
+		return -1;
+	memset(s, 0, sizeof(*s));
+	s->in_octets = odp_atomic_load_u64(&e->in_octets);
+	s->in_packets = odp_atomic_load_u64(&e->in_packets);
+	s->in_discards = odp_atomic_load_u64(&e->in_discards);
+	s->in_errors = odp_atomic_load_u64(&e->in_errors);
+	s->out_octets = odp_atomic_load_u64(&e->out_octets);
+	s->out_packets = odp_atomic_load_u64(&e->out_packets);
+	s->out_discards = odp_atomic_load_u64(&e->out_discards);
+	return 0;
+}
+
+int odp_pktio_stats_reset(odp_pktio_t h)
+{
+	rt_pktio_t *e = get_pk(h);
+
+	if (!e)
+		return -1;
+	odp_atomic_init_u64(&e->in_octets, 0);
+	odp_atomic_init_u64(&e->in_packets, 0);
+	odp_atomic_init_u64(&e->in_discards, 0);
+	odp_atomic_init_u64(&e->in_errors, 0);
+	odp_atomic_init_u64(&e->out_octets, 0);
+	odp_atomic_init_u64(&e->out_packets, 0);
+	odp_atomic_init_u64(&e->out_discards, 0);
+	return 0;
+}
+
+int odp_pktio_info(odp_pktio_t h, odp_pktio_info_t *info)
+{
+	rt_pktio_t *e = get_pk(h);
+
+	if (!e || !info)
+		return -1;
+	info->name = e->name;
+	info->drv_name = e->drv == DRV_PCAP ? "pcap" : e->drv == DRV_LOOP ? "loop" : "null";
+	info->pool = e->pool;
+	info->param = e->param;
+	return 0;
+}
+
+int odp_pktio_index(odp_pktio_t h)
+{
+	return get_pk(h) ? (int)((uintptr_t)h - 1) : -1;
+}
+
+uint64_t odp_pktio_to_u64(odp_pktio_t h)
+{
+	return (uint64_t)(uintptr_t)h;
+}
+
+void odp_pktio_print(odp_pktio_t h)
+{
+	rt_pktio_t *e = get_pk(h);
+	odp_pktio_stats_t s;
+
+	if (!e)
+		return;
+	odp_pktio_stats(h, &s);
+	printf("Pktio info\n----------\n  name            %s\n  driver          %s\n"
+	       "  classifier      %s\n  frames (pcap)   %u\n  in_packets      %" PRIu64 "\n"
+	       "  in_errors       %" PRIu64 "\n  in_discards     %" PRIu64 "\n\n", e->name,
+	       e->drv == DRV_PCAP ? "pcap" : e->drv == DRV_LOOP ? "loop" : "null",
+	       e->cls_enabled ? "enabled (GPU)" : "disabled", e->nframes, s.in_packets,
+	       s.in_errors, s.in_discards);
+}
+
+/* Build extension: 1 when the driver has no more input and no receive burst
+ * is in flight (pcap past EOF, loop queue empty); 0 otherwise; -1 bad handle. */
+int odp_amd_pktio_rx_idle(odp_pktio_t h)
+{
+	rt_pktio_t *e = get_pk(h);
+	int idle;
+
+	if (!e)
+		return -1;
+	odp_spinlock_lock(&e->rxl);
+	if (e->drv == DRV_PCAP)
+		idle = e->eof || e->nframes == 0 || (e->next >= e->nframes && e->loops == 1);
+	else if (e->drv == DRV_LOOP)
+		idle = ((rt_queue_t *)(void *)e->loopq)->count == 0;
+	else
+		idle = 1;
+	odp_spinlock_unlock(&e->rxl);
+	return idle;
+}

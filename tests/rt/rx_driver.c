@@ -1,0 +1,351 @@
+/*
+ * rx_driver.c -- test driver for the ODP runtime + GPU receive path.
+ *
+ * Replays a rule program (text form of odp_amd.rules programs, written by
+ * tests/rt_helpers.py) through the odp_cls_* API, opens a pktio, runs the
+ * receive path and prints every packet that reaches a queue, in arrival
+ * order per queue, with its metadata.  tests/test_runtime*.py compare the
+ * output against the CPU oracle.  Test infrastructure only.
+ *
+ * usage: rx_driver <pktio> <rules|-> <sched|direct|queue> <layer 0-4>
+ *                  <cos_pools 0|1> <cls 0|1> [source pcap for loop]
+ *   <pktio> = "pcap:in=FILE..." or "loop" (then the frames of the source
+ *   pcap are read through a second, parse-less pcap pktio and sent into the
+ *   loop interface).
+ * output lines:
+ *   P <queue> <pool> <in_flags> <err> <l3> <l4> <cos> <mark> <hex frame>
+ *   S <in_packets> <in_errors> <in_discards> <in_octets>
+ *   Q <cos> <slot> <packets> <discards>     (odp_cls_queue_stats)
+ */
+#define _GNU_SOURCE
+#include <inttypes.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "odp_api.h"
+
+#define MAX_COS 256
+#define MAX_PMR 8192
+
+static odp_cos_t cos_h[MAX_COS];
+static odp_queue_t cos_q[MAX_COS];
+static odp_pool_t cos_pool[MAX_COS];
+static char cos_name[MAX_COS][ODP_COS_NAME_LEN];
+static int ncos;
+static odp_pmr_t pmr_h[MAX_PMR];
+static int npmr;
+
+static int hexval(char c)
+{
+	return c >= '0' && c <= '9' ? c - '0' : c >= 'a' && c <= 'f' ? c - 'a' + 10 : -1;
+}
+
+static int unhex(const char *s, uint8_t *out, int max)
+{
+	int n = 0;
+
+	if (strcmp(s, "-") == 0)
+		return 0;
+	while (s[0] && s[1] && n < max) {
+		out[n++] = (uint8_t)(hexval(s[0]) << 4 | hexval(s[1]));
+		s += 2;
+	}
+	return n;
+}
+
+static odp_pool_t mkpool(const char *name)
+{
+	odp_pool_param_t p;
+
+	odp_pool_param_init(&p);
+	p.type = ODP_POOL_PACKET;
+	p.pkt.len = 1856;
+	p.pkt.seg_len = 1856;
+	p.pkt.num = 20000;
+	return odp_pool_create(name, &p);
+}
+
+static int replay(FILE *f, odp_pktio_t pktio, int cos_pools)
+{
+	char line[65536];
+
+	while (fgets(line, sizeof(line), f)) {
+		char *save = NULL, *tok = strtok_r(line, " \n", &save);
+
+		if (!tok)
+			continue;
+		if (strcmp(tok, "cos") == 0) {
+			/* cos <name> <action> <num_queue> <hash_proto> <stats> */
+			char *name = strtok_r(NULL, " \n", &save);
+			int action = atoi(strtok_r(NULL, " \n", &save));
+			int nq = atoi(strtok_r(NULL, " \n", &save));
+			unsigned hp = (unsigned)strtoul(strtok_r(NULL, " \n", &save), NULL, 0);
+			int stats = atoi(strtok_r(NULL, " \n", &save));
+			odp_cls_cos_param_t cp;
+			odp_queue_param_t qp;
+
+			odp_cls_cos_param_init(&cp);
+			odp_queue_param_init(&qp);
+			qp.type = ODP_QUEUE_TYPE_SCHED;
+			cp.action = action ? ODP_COS_ACTION_DROP : ODP_COS_ACTION_ENQUEUE;
+			cp.stats_enable = stats;
+			cp.num_queue = (uint32_t)nq;
+			snprintf(cos_name[ncos], ODP_COS_NAME_LEN, "%s", name);
+			if (!action) {
+				if (nq > 1) {
+					cp.queue_param = qp;
+					cp.hash_proto.all_bits = hp;
+				} else {
+					cos_q[ncos] = odp_queue_create(name, &qp);
+					cp.queue = cos_q[ncos];
+				}
+				if (cos_pools) {
+					char pn[ODP_POOL_NAME_LEN];
+
+					snprintf(pn, sizeof(pn), "%.24sPool", name);
+					cos_pool[ncos] = mkpool(pn);
+					cp.pool = cos_pool[ncos];
+				}
+			}
+			cos_h[ncos++] = odp_cls_cos_create(name, &cp);
+		} else if (strcmp(tok, "pmr") == 0) {
+			/* pmr <src> <dst> <mark> <nterms> {<term> <val> <mask> <offset>} */
+			int src = atoi(strtok_r(NULL, " \n", &save));
+			int dst = atoi(strtok_r(NULL, " \n", &save));
+			uint64_t mark = strtoull(strtok_r(NULL, " \n", &save), NULL, 0);
+			int nt = atoi(strtok_r(NULL, " \n", &save));
+			odp_pmr_param_t t[8];
+			uint8_t val[8][16], msk[8][16];
+			odp_pmr_create_opt_t opt;
+
+			for (int i = 0; i < nt && i < 8; i++) {
+				odp_cls_pmr_param_init(&t[i]);
+				t[i].term = (odp_cls_pmr_term_t)atoi(strtok_r(NULL, " \n", &save));
+				t[i].val_sz = (uint32_t)unhex(strtok_r(NULL, " \n", &save), val[i], 16);
+				unhex(strtok_r(NULL, " \n", &save), msk[i], 16);
+				t[i].offset = (uint32_t)atoi(strtok_r(NULL, " \n", &save));
+				t[i].match.value = val[i];
+				t[i].match.mask = msk[i];
+			}
+			odp_cls_pmr_create_opt_init(&opt);
+			opt.terms = t;
+			opt.num_terms = nt;
+			opt.mark = mark;
+			pmr_h[npmr++] = odp_cls_pmr_create_opt(&opt, cos_h[src], cos_h[dst]);
+		} else if (strcmp(tok, "pmr_destroy") == 0) {
+			odp_cls_pmr_destroy(pmr_h[atoi(strtok_r(NULL, " \n", &save))]);
+		} else if (strcmp(tok, "cos_destroy") == 0) {
+			odp_cos_destroy(cos_h[atoi(strtok_r(NULL, " \n", &save))]);
+		} else if (strcmp(tok, "default") == 0 || strcmp(tok, "error") == 0) {
+			int i = atoi(strtok_r(NULL, " \n", &save));
+			odp_cos_t c = i < 0 ? ODP_COS_INVALID : cos_h[i];
+
+			if (tok[0] == 'd')
+				odp_pktio_default_cos_set(pktio, c);
+			else
+				odp_pktio_error_cos_set(pktio, c);
+		}
+	}
+	return 0;
+}
+
+static const char *qname(odp_queue_t q)
+{
+	odp_queue_info_t info;
+
+	return odp_queue_info(q, &info) == 0 ? info.name : "?";
+}
+
+static const char *poolname(odp_pool_t p)
+{
+	odp_pool_info_t info;
+
+	return odp_pool_info(p, &info) == 0 ? info.name : "?";
+}
+
+static void print_pkt(const char *q, odp_packet_t pkt)
+{
+	uint32_t len = odp_packet_len(pkt);
+	const uint8_t *d = odp_packet_data(pkt);
+	uint64_t fl = 0;
+
+	/* reassemble the input_flags word from the packet_flags.h accessors */
+	static int (*const fn[])(odp_packet_t) = {
+		NULL, odp_packet_has_flow_hash, odp_packet_has_ts, odp_packet_has_l2,
+		odp_packet_has_l3, odp_packet_has_l4, odp_packet_has_eth, odp_packet_has_eth_bcast,
+		odp_packet_has_eth_mcast, odp_packet_has_jumbo, odp_packet_has_vlan,
+		odp_packet_has_vlan_qinq, odp_packet_has_arp, odp_packet_has_ipv4,
+		odp_packet_has_ipv6, odp_packet_has_ip_bcast, odp_packet_has_ip_mcast,
+		odp_packet_has_ipfrag, odp_packet_has_ipopt, odp_packet_has_ipsec, NULL, NULL,
+		odp_packet_has_udp, odp_packet_has_tcp, odp_packet_has_sctp, odp_packet_has_icmp };
+	for (unsigned b = 0; b < sizeof(fn) / sizeof(fn[0]); b++)
+		if (fn[b] && fn[b](pkt))
+			fl |= 1ull << b;
+	printf("P %s %s %" PRIx64 " %d %u %u %" PRIu64 " %u ", q, poolname(odp_packet_pool(pkt)), fl,
+	       odp_packet_has_error(pkt), odp_packet_l3_offset(pkt), odp_packet_l4_offset(pkt),
+	       odp_packet_cls_mark(pkt), len);
+	for (uint32_t i = 0; i < len; i++)
+		printf("%02x", d[i]);
+	printf("\n");
+}
+
+int main(int argc, char *argv[])
+{
+	odp_instance_t inst;
+	odp_pktio_param_t pp;
+	odp_pktin_queue_param_t iq;
+	odp_pktout_queue_param_t oq;
+	odp_pktio_config_t cfg;
+	const char *mode;
+	int layer, cos_pools, cls;
+
+	if (argc < 7) {
+		fprintf(stderr, "usage: %s <pktio> <rules|-> <sched|direct|queue> <layer> "
+			"<cos_pools> <cls> [source pcap]\n", argv[0]);
+		return 2;
+	}
+	mode = argv[3];
+	layer = atoi(argv[4]);
+	cos_pools = atoi(argv[5]);
+	cls = atoi(argv[6]);
+	if (odp_init_global(&inst, NULL, NULL) || odp_init_local(inst, ODP_THREAD_CONTROL))
+		return 3;
+	odp_schedule_config(NULL);
+	odp_pool_t pool = mkpool("pktio_pool");
+
+	odp_pktio_param_init(&pp);
+	pp.in_mode = strcmp(mode, "sched") == 0 ? ODP_PKTIN_MODE_SCHED :
+		     strcmp(mode, "queue") == 0 ? ODP_PKTIN_MODE_QUEUE : ODP_PKTIN_MODE_DIRECT;
+	odp_pktio_t pktio = odp_pktio_open(argv[1], pool, &pp);
+
+	if (pktio == ODP_PKTIO_INVALID)
+		return 4;
+	odp_pktin_queue_param_init(&iq);
+	iq.classifier_enable = cls;
+	if (odp_pktin_queue_config(pktio, &iq))
+		return 5;
+	odp_pktout_queue_param_init(&oq);
+	if (odp_pktout_queue_config(pktio, &oq))
+		return 5;
+	if (!getenv("RX_NO_PROMISC"))
+		odp_pktio_promisc_mode_set(pktio, 1);
+	odp_pktio_config_init(&cfg);
+	cfg.parser.layer = (odp_proto_layer_t)layer;
+	if (odp_pktio_config(pktio, &cfg))
+		return 6;
+	if (strcmp(argv[2], "-") != 0) {
+		FILE *f = fopen(argv[2], "r");
+
+		if (!f)
+			return 7;
+		replay(f, pktio, cos_pools);
+		fclose(f);
+	}
+	if (odp_pktio_start(pktio))
+		return 8;
+
+	/* loop: feed the source frames through a parse-less pcap pktio */
+	if (strncmp(argv[1], "loop", 4) == 0 && argc > 7) {
+		char src[512];
+		odp_pktio_param_t sp;
+		odp_pktio_config_t sc;
+		odp_pktin_queue_t inq;
+		odp_pktout_queue_t outq;
+		odp_packet_t pk[256];
+		int n;
+
+		snprintf(src, sizeof(src), "pcap:in=%s", argv[7]);
+		odp_pktio_param_init(&sp);
+		odp_pktio_t sio = odp_pktio_open(src, pool, &sp);
+
+		if (sio == ODP_PKTIO_INVALID || odp_pktin_queue_config(sio, NULL))
+			return 9;
+		odp_pktio_promisc_mode_set(sio, 1);
+		odp_pktio_config_init(&sc);
+		sc.parser.layer = ODP_PROTO_LAYER_NONE;
+		odp_pktio_config(sio, &sc);
+		if (odp_pktio_start(sio) || odp_pktin_queue(sio, &inq, 1) != 1 ||
+		    odp_pktout_queue(pktio, &outq, 1) < 1)
+			return 9;
+		while ((n = odp_pktin_recv(inq, pk, 256)) > 0)
+			if (odp_pktout_send(outq, pk, n) != n)
+				return 10;
+		odp_pktio_stop(sio);
+		odp_pktio_close(sio);
+	}
+
+	if (pp.in_mode == ODP_PKTIN_MODE_DIRECT) {
+		odp_pktin_queue_t inq;
+		odp_packet_t pk[512];
+		int n, idle = 0;
+
+		if (odp_pktin_queue(pktio, &inq, 1) != 1)
+			return 11;
+		while (idle < 3) {
+			n = odp_pktin_recv(inq, pk, 512);
+			for (int i = 0; i < n; i++) {
+				print_pkt("pktin", pk[i]);
+				odp_packet_free(pk[i]);
+			}
+			idle = (n == 0 && odp_amd_pktio_rx_idle(pktio) == 1) ? idle + 1 : 0;
+		}
+		/* classified packets went to CoS queues: drain them */
+		for (;;) {
+			odp_event_t ev[64];
+			odp_queue_t from;
+
+			n = odp_schedule_multi(&from, ODP_SCHED_NO_WAIT, ev, 64);
+			if (n <= 0)
+				break;
+			for (int i = 0; i < n; i++) {
+				print_pkt(qname(from), odp_packet_from_event(ev[i]));
+				odp_event_free(ev[i]);
+			}
+		}
+	} else {
+		int idle = 0;
+		odp_queue_t pin = ODP_QUEUE_INVALID;
+
+		odp_pktin_event_queue(pktio, &pin, 1);
+		while (idle < 3) {
+			odp_event_t ev[64];
+			odp_queue_t from;
+			int n;
+
+			if (pp.in_mode == ODP_PKTIN_MODE_QUEUE) {
+				n = odp_queue_deq_multi(pin, ev, 64);
+				from = pin;
+				if (n <= 0)
+					n = odp_schedule_multi(&from, ODP_SCHED_NO_WAIT, ev, 64);
+			} else {
+				n = odp_schedule_multi(&from, ODP_SCHED_NO_WAIT, ev, 64);
+			}
+			for (int i = 0; i < n; i++) {
+				print_pkt(qname(from), odp_packet_from_event(ev[i]));
+				odp_event_free(ev[i]);
+			}
+			idle = (n <= 0 && odp_amd_pktio_rx_idle(pktio) == 1) ? idle + 1 : 0;
+		}
+	}
+	odp_pktio_stats_t st;
+
+	odp_pktio_stats(pktio, &st);
+	printf("S %" PRIu64 " %" PRIu64 " %" PRIu64 " %" PRIu64 "\n", st.in_packets, st.in_errors,
+	       st.in_discards, st.in_octets);
+	for (int c = 0; c < ncos; c++) {
+		odp_queue_t qs[32];
+		uint32_t nq = odp_cls_cos_queues(cos_h[c], qs, 32);
+
+		for (uint32_t s = 0; s < nq && s < 32; s++) {
+			odp_cls_queue_stats_t qs_;
+
+			if (odp_cls_queue_stats(cos_h[c], qs[s], &qs_) == 0)
+				printf("Q %s %u %" PRIu64 " %" PRIu64 "\n", cos_name[c], s, qs_.packets,
+				       qs_.discards);
+		}
+	}
+	odp_pktio_stop(pktio);
+	odp_pktio_close(pktio);
+	return 0;
+}
