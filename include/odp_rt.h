@@ -71,7 +71,7 @@ typedef uint64_t odp_instance_t;
 #define ODP_COS_NAME_LEN    32
 #define ODP_POOL_NAME_LEN   32
 #define ODP_QUEUE_NAME_LEN  32
-#define ODP_PKTIO_NAME_LEN  64
+#define ODP_PKTIO_NAME_LEN  256   /* PKTIO_NAME_LEN, odp_packet_io_internal.h:51 */
 #define ODP_SHM_NAME_LEN    32
 #define ODP_THREAD_COUNT_MAX 256
 #define ODP_PKTIN_MAX_QUEUES  64

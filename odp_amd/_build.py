@@ -81,17 +81,22 @@ TEST_BIN = os.path.join(ROOT, "tests", "_bin")
 
 def build_test_drivers(force: bool = False):
     """Test-only C drivers of the runtime (tests/rt/*.c -> tests/_bin/)."""
-    src = os.path.join(ROOT, "tests", "rt", "rx_driver.c")
-    if not os.path.exists(src):
-        return None
-    os.makedirs(TEST_BIN, exist_ok=True)
-    out = os.path.join(TEST_BIN, "rx_driver")
-    if not force and not _stale(out, [src, os.path.join(PKG, "libodp_cls.so"),
-                                      os.path.join(INC, "odp_rt.h")]):
-        return None
-    _run(["gcc", "-O2", "-std=gnu11", "-Wall", "-I", INC, "-o", out, src, "-L", PKG,
-          "-lodp_cls", "-Wl,-rpath,$ORIGIN/" + os.path.relpath(PKG, TEST_BIN), "-lpthread"])
-    return out
+    built = None
+    deps = [os.path.join(PKG, "libodp_cls.so"), os.path.join(PKG, "libodph.so"),
+            os.path.join(INC, "odp_rt.h"), os.path.join(INC, "odp", "helper", "odph_api.h")]
+    for name in ("rx_driver", "rt_unit"):
+        src = os.path.join(ROOT, "tests", "rt", name + ".c")
+        if not os.path.exists(src):
+            continue
+        os.makedirs(TEST_BIN, exist_ok=True)
+        out = os.path.join(TEST_BIN, name)
+        if not force and not _stale(out, [src] + deps):
+            continue
+        _run(["gcc", "-O2", "-std=gnu11", "-Wall", "-I", INC, "-o", out, src, "-L", PKG,
+              "-lodph", "-lodp_cls", "-Wl,-rpath,$ORIGIN/" + os.path.relpath(PKG, TEST_BIN),
+              "-lpthread"])
+        built = out
+    return built
 
 
 REF_EXAMPLE = "/root/reference/example/classifier/odp_classifier.c"

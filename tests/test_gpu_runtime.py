@@ -1,0 +1,123 @@
+"""End-to-end receive path on the GPU through the ODP runtime subset: frames
+enter a pcap or loop pktio, are parsed + classified in GPU bursts
+(odp_amd_cls_classify_host -> mi_cls_kernel) and land in CoS queues; the
+packets every queue delivers (order, pool, input flags, error bit, l3/l4
+offsets, cls mark, bytes) and the pktio / queue counters must be exactly what
+the reference receive path produces, derived from the CPU oracle
+(tests/rt_helpers.expected).  Also runs the reference's example/classifier,
+compiled unchanged against this build, with its own CI arguments
+(example/classifier/odp_classifier_run.sh,
+platform/linux-generic/test/example/classifier/pktio_env:21-23).
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from odp_amd import rules as R
+from tests import rt_helpers as H
+from tests import zoo
+
+pytestmark = pytest.mark.gpu
+
+UDP64 = os.path.join(H.ROOT, "tests", "golden", "udp64.pcap")
+
+
+def _run_case(tmp_path, prog, frames, mode="sched", pktio="pcap", cos_pools=1, layer=4, cls=1,
+              burst=None):
+    pc = str(tmp_path / "in.pcap")
+    H.write_pcap(pc, frames)
+    rules = str(tmp_path / "rules.txt")
+    H.write_rules(rules, prog)
+    env = {"ODP_AMD_RX_BURST": str(burst)} if burst else None
+    if pktio == "loop":
+        got = H.run_driver("loop", rules, mode, layer, cos_pools, cls, src=pc, env=env)
+    else:
+        got = H.run_driver(f"pcap:in={pc}", rules, mode, layer, cos_pools, cls, env=env)
+    exp = H.expected(prog, frames, cos_pools, cls, layer)
+    H.compare(got, exp)
+    return got
+
+
+def test_example_classifier_udp64(built, gpu):
+    """The reference's own acceptance run: 100 packets to queue1, 100 to
+    DefaultCos, exit status 0."""
+    if not os.path.exists(H.EXAMPLE):
+        pytest.skip("example binary not built")
+    r = subprocess.run([H.EXAMPLE, "-t", "1", "-i", f"pcap:in={UDP64}", "-m", "0", "-p",
+                        "ODP_PMR_SIP_ADDR:10.10.10.0:0xFFFFFF00:queue1", "-P", "-C",
+                        "queue1:100", "-C", "DefaultCos:100"],
+                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=90,
+                       cwd="/tmp")
+    assert r.returncode == 0, r.stdout[-3000:]
+    # the statistics row: "<queue> <pool>|" per policy, then total
+    rows = [ln for ln in r.stdout.splitlines() if ln.count("|") >= 2 and ln[:1].isdigit()]
+    assert rows, r.stdout[-3000:]
+    cells = [c.split() for c in rows[-1].split("|")[:2]]
+    assert [int(x) for x in cells[0]] == [100, 100]   # queue1: queue, pool
+    assert [int(x) for x in cells[1]] == [100, 100]   # DefaultCos
+    assert "Exit" in r.stdout
+
+
+def test_example_classifier_two_workers_dmac(built, gpu):
+    """Two worker threads, a DMAC rule, no dedicated CoS pools (-d 0)."""
+    if not os.path.exists(H.EXAMPLE):
+        pytest.skip("example binary not built")
+    r = subprocess.run([H.EXAMPLE, "-t", "1", "-c", "2", "-d", "0", "-i", f"pcap:in={UDP64}",
+                        "-m", "0", "-p", "ODP_PMR_DMAC:02-00-00-00-00-02:ffffffffffff:mac",
+                        "-P", "-C", "mac:200"],
+                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=90,
+                       cwd="/tmp")
+    assert r.returncode == 0, r.stdout[-3000:]
+
+
+@pytest.mark.parametrize("mode", ["sched", "direct", "queue"])
+def test_rx_zoo_everything(built, gpu, tmp_path, mode):
+    frames = H.pcap_frames([f for _, f in zoo.all_frames()])
+    _run_case(tmp_path, zoo.prog_everything(), frames, mode)
+
+
+def test_rx_zoo_shared_pool(built, gpu, tmp_path):
+    frames = H.pcap_frames([f for _, f in zoo.all_frames()])
+    _run_case(tmp_path, zoo.prog_everything(), frames, cos_pools=0)
+
+
+def test_rx_loop_pktio(built, gpu, tmp_path):
+    frames = H.pcap_frames([f for _, f in zoo.all_frames()])
+    _run_case(tmp_path, zoo.prog_everything(), frames, pktio="loop")
+
+
+def test_rx_deletes_and_drops(built, gpu, tmp_path):
+    frames = H.pcap_frames([f for _, f in zoo.all_frames()])
+    _run_case(tmp_path, zoo.prog_deletes(), frames)
+    _run_case(tmp_path, zoo.prog_no_default(), frames)
+
+
+@pytest.mark.parametrize("layer", [0, 1, 2, 3])
+def test_rx_parse_layers_no_classifier(built, gpu, tmp_path, layer):
+    """Classifier disabled: packets go to the pktin queue parsed up to the
+    configured layer (odp_packet_io.c:675-677, odp_parse.c:372-414)."""
+    frames = H.pcap_frames([f for _, f in zoo.all_frames()])
+    _run_case(tmp_path, [], frames, cls=0, layer=layer)
+
+
+def test_rx_random_programs_small_bursts(built, gpu, tmp_path):
+    """Random CoS graphs + fuzzed frames, with 37-packet GPU bursts so that
+    enqueue runs straddle burst boundaries."""
+    rng = np.random.default_rng(1234)
+    base = [f for _, f in zoo.all_frames()]
+    for it in range(3):
+        frames = H.pcap_frames(base + zoo.mutate_frames(rng, base, 300))
+        prog = zoo.random_program(rng, base)
+        if any(op[0] == "cos" and " " in op[1] for op in prog):
+            continue
+        _run_case(tmp_path, prog, frames, burst=37)
+
+
+def test_rx_config2_traffic(built, gpu, tmp_path):
+    """BASELINE config 2 traffic (16 SIP /24 rules) through the pcap pktio."""
+    b, prog = R.config2(20000)
+    frames = [b.frame(i) for i in range(b.n)]
+    got = _run_case(tmp_path, prog, frames)
+    assert sum(len(v) for v in got[0].values()) == 20000
