@@ -137,7 +137,7 @@ def expected(prog, frames, cos_pools=1, cls=1, layer=4, pktin_queue="odp-pktin-0
         l3, l4 = int(r["l3_offset"]), int(r["l4_offset"])
         if layer == 0:
             fl, err, l3, l4 = 0, 0, 0xFFFF, 0xFFFF
-        elif layer < 4:     # odp_parse.c:372-414: cut below L4
+        elif layer < 3:     # L2 (1) and L3 (2) cut the parse (odp_parse.c:372-414)
             if out == R.OUT_PARSE_DROP:
                 out = R.OUT_DISCARD
             if layer == 1:
