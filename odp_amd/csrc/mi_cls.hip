@@ -691,24 +691,27 @@ enum { DH_MAGIC = 0, DH_NCOS, DH_DEFAULT, DH_ERROR, DH_DEFAULT_VALID, DH_USED, D
 #define BV_EMPTY 0xFFFFFFFFu
 #define BV_NONE 0xFFFFFFFEu
 
-// Bit-vector (BV) block of a CoS, used when its rules fall into at most
-// BV_MAX_CLS key classes.  A key class is one (term kind, mask[, offset,
-// size]) combination; for every class the block holds a hash table
-// key -> bitmap row over the CoS's rules (bit r = rule r's terms of that
-// class all equal the key, or rule r has no term of that class), row 0 being
-// the "no term of this class" row used when the packet lacks the field or
-// its key is in no rule.  A packet's matching rules are the AND of its rows;
-// the lowest set bit is the first rule in scan order whose every term
-// matches -- exactly the rule match_pmr_cos picks
-// (odp_classification.c:1631-1650).  With a single class the AND is a no-op,
-// so the block is DIRECT: a table slot holds the first live rule of its row
-// and class word 2 the first live rule of row 0 (BV_NONE = no rule).
-//   bv[0] = W (32-bit words per row, 0 when direct), bv[1] = #classes,
-//   bv[2] = alive row, bv[3] = result words (dst | leaf<<8 | mark<<16, one per
-//   rule; leaf = the destination CoS has no rules, so the descent ends there)
-//   bv[4 + 16 k ...] class k: kind, nkey, row-0 first rule (direct), offset,
-//                    size, mask[4], table mask, table offset, rows offset
-//   table slot: nkey key words + row index / first rule (BV_EMPTY = free)
+// Classification block of a CoS ("BV" block for historical reasons), used
+// when its rules fall into at most BV_MAX_CLS key classes (a key class is one
+// (term kind, mask[, offset, size]) combination).  build_bv() explains the
+// two modes; the layout (word indices into the hot region) is:
+//   b[0] mode (0 direct, 1 candidate, 2 bitmap), b[1] #classes, b[2] result words
+//   (dst | leaf<<8 | mark<<16 per rule; leaf = the destination CoS has no
+//   rules, so the descent ends there), b[3] first rule without a classified
+//   term (BV_NONE: none), b[4] rule records (bitmap: alive row), b[5]
+//   record words
+//   b[8 + 16 k ...] class k: kind, nkey, miss value (direct: first rule,
+//                   bitmap: row), offset, size, mask[4], #slots, table
+//                   offset, cuckoo multipliers m1, m2, list base
+//   table slot (nkey + 1 words): key words, value (0: empty)
+//     direct: 1 + first live rule with this key or without a term of the
+//             class (BV_EMPTY: none)
+//     bitmap: the 32-bit row of rules with this key or without a term
+//     candidate: key id | list length << 12 | list offset << 20; the list
+//             holds the rules filed under this key, in scan order
+//   rule record (candidate, 1 + ceil(#classes / 2) words): constrained-
+//             class mask (bit 31: never holds), then the required key id of
+//             class c in half c & 1 of word 1 + c / 2
 
 __device__ __forceinline__ bool eq1(uint32_t x, uint32_t m, uint32_t v)
 {
@@ -742,17 +745,15 @@ __device__ __forceinline__ bool term_ok(cword_t prog, uint32_t &q, const Pkt &k,
 	return ok;
 }
 
-__device__ __forceinline__ uint32_t bv_hash(const uint32_t k[4])
+__device__ __forceinline__ uint32_t bv_fold(const uint32_t k[4])
 {
 	uint32_t h = k[0] * 0x9E3779B1u ^ k[1] * 0x85EBCA77u ^ k[2] * 0xC2B2AE3Du ^ k[3] * 0x27D4EB2Fu;
-	h ^= h >> 15;
-	h *= 0x2C1B3C6Du;
-	h ^= h >> 12;
-	return h;
+	return h ^ (h >> 15);
 }
 
-// Word readers of a BV block: wave-uniform blocks are read with scalar loads
-// from HBM (DescU), per-lane blocks from the hot region (LDS or HBM, DescL).
+// Word readers of a classification block: wave-uniform blocks are read with
+// scalar loads from HBM (DescU), per-lane blocks from the hot region (LDS or
+// HBM, DescL).
 struct DescU {
 	cword_t p;
 	__device__ __forceinline__ uint32_t operator()(uint32_t i) const { return p[i]; }
@@ -765,7 +766,7 @@ template <typename T> struct DescL {
 	__device__ __forceinline__ DescL at(uint32_t o) const { return DescL{ p, b + o }; }
 };
 
-// Key of a packet for one BV class: the masked field the class's terms
+// Key of a packet for one class: the masked field the class's terms
 // compare, and whether the packet has that field at all (the term's gate).
 template <typename D>
 __device__ __forceinline__ bool bv_key(const D &cr, const Pkt &k, const Parsed &p, const Fields &x,
@@ -792,85 +793,125 @@ __device__ __forceinline__ bool bv_key(const D &cr, const Pkt &k, const Parsed &
 	return present;
 }
 
-// Probe a class's open-addressing table for the key of every lane in `act`;
-// returns the slot's value (row index / first rule) or `miss` when the key
-// is absent.  The probe loop runs until no lane of the wave is still
-// searching; per-lane state lives in VGPRs and is updated by selects.
-template <typename T>
-__device__ __forceinline__ uint32_t bv_probe(T H, uint32_t tbl, uint32_t tmask, uint32_t nk,
-					     const uint32_t key[4], bool act, uint32_t miss)
+// Two-choice cuckoo lookup: the key sits in slot s1 or s2 (both read at
+// once, no probe loop).  A slot is nk key words and a value word; an empty
+// slot has key words 0 and value 0, so "key equal and value non-zero" is a
+// hit.  Returns the hit slot's value, or 0 on a miss.
+template <typename D, typename T>
+__device__ __forceinline__ uint32_t bv_lookup(const D &cr, T H, const uint32_t key[4], bool act)
 {
-	uint32_t h = bv_hash(key) & tmask, val = miss;
-	uint32_t searching = act ? 1u : 0u;
-	for (uint32_t probe = 0; probe <= tmask; ++probe) {
-		if (__ballot(searching != 0u) == 0ull)
-			break;
-		const uint32_t sl = tbl + h * (nk + 1u);
-		const uint32_t rw = H[sl + nk];
-		bool eq = H[sl] == key[0];
+	const uint32_t nk = cr(1), ns = cr(9), tbl = cr(10);
+	const uint32_t f = bv_fold(key);
+	const uint32_t sw = nk + 1u;
+	uint32_t val = 0;
+#pragma unroll
+	for (uint32_t s = 0; s < 2; ++s) {
+		const uint32_t a = tbl + __umulhi(f * cr(11u + s), ns) * sw;
+		bool e = H[a] == key[0];
 		if (nk > 1)
-			eq = eq && H[sl + 1] == key[1];
+			e = e && H[a + 1] == key[1];
 		if (nk > 2)
-			eq = eq && H[sl + 2] == key[2] && H[sl + 3] == key[3];
-		const bool empty = rw == BV_EMPTY;
-		const bool found = searching != 0u && !empty && eq;
-		val = found ? rw : val;
-		searching = (searching != 0u && !empty && !eq) ? 1u : 0u;
-		h = (h + 1u) & tmask;
+			e = e && H[a + 2] == key[2] && H[a + 3] == key[3];
+		const uint32_t v = H[a + nk];
+		val = (act && e && v != 0u) ? v : val;
 	}
 	return val;
 }
 
-// Bit-vector evaluation of one CoS for the lanes in `act`.  `blk` reads the
-// CoS's BV block (wave-uniform or per lane); H is the hot region the table
-// offsets index.  On return, lanes of `act` with a matching rule have
-// done = true and the rule's destination CoS / mark in nxt / nmark.
+// Classification block evaluation of one CoS for the lanes in `act`
+// (see build_bv for the two modes).  `blk` reads the CoS's block (wave-
+// uniform or per lane); H is the hot region the block's offsets index.  On
+// return, lanes of `act` with a matching rule have hit = 1 and the rule's
+// destination CoS / mark / leaf bit in nxt / nmark / nleaf.
 template <typename D, typename T>
 __device__ __forceinline__ void bv_eval(const D &blk, T H, bool act, const Pkt &k, const Parsed &p,
 					const Fields &x, uint32_t &hit, uint32_t &nxt, uint32_t &nmark,
 					uint32_t &nleaf)
 {
-	const uint32_t Wd = blk(0), ncls = blk(1), alive = blk(2), res = blk(3);
+	const uint32_t mode = blk(0), ncls = blk(1), res = blk(2);
 	uint32_t first = BV_NONE;
-	if (Wd == 0u) {
-		// direct: one class, the slot holds the first live rule of its row
-		const D cr = blk.at(4u);
+	if (mode == 0u) {
+		// direct: one class, the slot holds 1 + the first live rule of its
+		// key (BV_EMPTY: none); a miss takes the block's "no term" rule
+		const D cr = blk.at(8u);
 		uint32_t key[4];
 		const bool present = bv_key(cr, k, p, x, key);
-		const uint32_t r0 = cr(2);
-		first = bv_probe(H, cr(10), cr(9), cr(1), key, act && present, r0);
-	} else {
-		uint32_t ridx[BV_MAX_CLS];
+		const uint32_t val = bv_lookup(cr, H, key, act && present);
+		first = val != 0u ? (val == BV_EMPTY ? BV_NONE : val - 1u) : cr(2);
+	} else if (mode == 2u) {
+		// bitmap: AND of the classes' 32-bit rows and the alive row
+		uint32_t acc = blk(4);
 #pragma unroll
 		for (uint32_t kc = 0; kc < BV_MAX_CLS; ++kc) {
-			ridx[kc] = 0;
 			if (kc < ncls) {
-				const D cr = blk.at(4u + BV_CLS_WORDS * kc);
+				const D cr = blk.at(8u + BV_CLS_WORDS * kc);
 				uint32_t key[4];
 				const bool present = bv_key(cr, k, p, x, key);
-				const uint32_t row = bv_probe(H, cr(10), cr(9), cr(1), key, act && present, 0u);
-				ridx[kc] = cr(11) + row * Wd;
+				const uint32_t val = bv_lookup(cr, H, key, act && present);
+				acc &= val != 0u ? val : cr(2);
 			}
 		}
-		uint32_t want = act ? 1u : 0u;
-		for (uint32_t w = 0; w < Wd; ++w) {
-			if (__ballot(want != 0u) == 0ull)
-				break;
-			uint32_t acc = H[alive + w];
+		first = acc != 0u ? (uint32_t)__builtin_ctz(acc) : BV_NONE;
+	} else {
+		// candidate: key id per class, then the candidates' records
+		const uint32_t rec0 = blk(4), rw = blk(5);
+		uint32_t v[BV_MAX_CLS], lb[BV_MAX_CLS];
 #pragma unroll
-			for (uint32_t kc = 0; kc < BV_MAX_CLS; ++kc)
-				if (kc < ncls)
-					acc &= H[ridx[kc] + w];
-			const bool f = want != 0u && acc != 0u;
-			first = f ? w * 32u + (uint32_t)__builtin_ctz(acc) : first;
-			want = (want != 0u && acc == 0u) ? 1u : 0u;
+		for (uint32_t kc = 0; kc < BV_MAX_CLS; ++kc) {
+			v[kc] = 0u;
+			lb[kc] = 0u;
+			if (kc < ncls) {
+				const D cr = blk.at(8u + BV_CLS_WORDS * kc);
+				uint32_t key[4];
+				const bool present = bv_key(cr, k, p, x, key);
+				v[kc] = bv_lookup(cr, H, key, act && present);
+				lb[kc] = cr(13);
+			}
+		}
+		first = blk(3);   // the first rule without a classified term
+#pragma unroll
+		for (uint32_t kc = 0; kc < BV_MAX_CLS; ++kc) {
+			if (kc < ncls) {
+				// value = key id | list length << 12 | list offset << 20
+				uint32_t j = 0, n = (v[kc] >> 12) & 0xffu;
+				const uint32_t lo = lb[kc] + (v[kc] >> 20);
+				for (;;) {
+					const bool more = act && j < n;
+					if (__ballot(more) == 0ull)
+						break;
+					if (more) {
+						const uint32_t r = H[lo + j];
+						bool ok = r < first;
+						if (ok) {
+							const uint32_t rec = rec0 + r * rw;
+							const uint32_t m = H[rec];
+							ok = (m >> 31) == 0u;
+#pragma unroll
+							for (uint32_t c = 0; c < BV_MAX_CLS; c += 2) {
+								if (c < ncls && ((m >> c) & 3u)) {
+									const uint32_t w = H[rec + 1u + (c >> 1)];
+									ok = ok && (!((m >> c) & 1u) ||
+										    (v[c] & 0xfffu) == (w & 0xffffu));
+									ok = ok && (!((m >> (c + 1)) & 1u) ||
+										    (v[c + 1] & 0xfffu) == (w >> 16));
+								}
+							}
+						}
+						first = ok ? r : first;
+						// lists are in scan order: the first candidate that
+						// holds, or reaches `first`, ends this list
+						n = (ok || r >= first) ? 0u : n;
+						++j;
+					}
+				}
+			}
 		}
 	}
 	const bool h = act && first != BV_NONE;
-	const uint32_t rw = H[res + (h ? first : 0u)];
-	nxt = h ? (rw & 0xffu) : nxt;
-	nleaf = h ? ((rw >> 8) & 1u) : nleaf;
-	nmark = h ? (rw >> 16) : nmark;
+	const uint32_t rw2 = H[res + (h ? first : 0u)];
+	nxt = h ? (rw2 & 0xffu) : nxt;
+	nleaf = h ? ((rw2 >> 8) & 1u) : nleaf;
+	nmark = h ? (rw2 >> 16) : nmark;
 	hit = h ? 1u : hit;
 }
 
@@ -1519,13 +1560,66 @@ struct ClassKey {
 
 typedef std::array<uint32_t, 4> Key4;
 
-static uint32_t host_bv_hash(const Key4 &k)
+// fold of a key's words (same as bv_fold on the device)
+static uint32_t host_bv_fold(const Key4 &k)
 {
+	// keep in step with bv_fold()
 	uint32_t h = k[0] * 0x9E3779B1u ^ k[1] * 0x85EBCA77u ^ k[2] * 0xC2B2AE3Du ^ k[3] * 0x27D4EB2Fu;
-	h ^= h >> 15;
-	h *= 0x2C1B3C6Du;
-	h ^= h >> 12;
-	return h;
+	return h ^ (h >> 15);
+}
+
+static uint32_t host_bucket(uint32_t fold, uint32_t mult, uint32_t nb)
+{
+	return (uint32_t)(((uint64_t)(uint32_t)(fold * mult) * nb) >> 32);
+}
+
+// Two-choice cuckoo table over `keys`: every key sits in slot s1 or s2 (a
+// lookup reads both at once, no probe loop).  Returns the slot of every key
+// and the slot count / multipliers used (load factor <= 45 %).
+static bool cuckoo_place(const std::vector<Key4> &keys, uint32_t &ns, uint32_t &m1, uint32_t &m2,
+			 std::vector<uint32_t> &slot_of)
+{
+	const uint32_t n = (uint32_t)keys.size();
+	std::vector<uint32_t> fold(n);
+	for (uint32_t i = 0; i < n; ++i)
+		fold[i] = host_bv_fold(keys[i]);
+	ns = (n * 20 + 8) / 9 + 2;
+	uint64_t rng = 0x9E3779B97F4A7C15ull ^ ((uint64_t)n << 17);
+	for (int grow = 0; grow < 8; ++grow, ns += ns / 4 + 1) {
+		for (int attempt = 0; attempt < 32; ++attempt) {
+			rng ^= rng << 13; rng ^= rng >> 7; rng ^= rng << 17;
+			m1 = (uint32_t)rng | 1u;
+			rng ^= rng << 13; rng ^= rng >> 7; rng ^= rng << 17;
+			m2 = (uint32_t)(rng >> 32) | 1u;
+			std::vector<int32_t> occ(ns, -1);
+			slot_of.assign(n, 0);
+			bool ok = true;
+			for (uint32_t i = 0; i < n && ok; ++i) {
+				uint32_t cur = i, pos = host_bucket(fold[i], m1, ns);
+				for (int kick = 0;; ++kick) {
+					if (occ[pos] < 0) {
+						occ[pos] = (int32_t)cur;
+						slot_of[cur] = pos;
+						break;
+					}
+					if (kick > 300) {
+						ok = false;
+						break;
+					}
+					const uint32_t ev = (uint32_t)occ[pos];
+					occ[pos] = (int32_t)cur;
+					slot_of[cur] = pos;
+					const uint32_t a1 = host_bucket(fold[ev], m1, ns);
+					const uint32_t a2 = host_bucket(fold[ev], m2, ns);
+					pos = a1 == pos ? a2 : a1;
+					cur = ev;
+				}
+			}
+			if (ok)
+				return true;
+		}
+	}
+	return false;
 }
 
 static bool class_of(const mi_term_t &t, ClassKey &ck)
@@ -1557,9 +1651,33 @@ static bool class_of(const mi_term_t &t, ClassKey &ck)
 	return true;
 }
 
-// Build the BV block of one CoS into `blk` (word offsets relative to the
-// start of the device program, base = blk's first word index).  Returns false
-// when the CoS needs more than BV_MAX_CLS classes (linear scan instead).
+// Build the classification block of one CoS into `blk` (word offsets are
+// relative to the start of the hot region; base = blk's first word index).
+// Returns false when the CoS needs more than BV_MAX_CLS key classes or its
+// candidate lists degenerate (the linear scan is used instead).
+//
+// Semantics (match_pmr_cos, odp_classification.c:1624-1667): the CoS's
+// result is the FIRST rule in scan order all of whose terms hold.  A rule's
+// terms are grouped by key class (term kind + mask [+ offset, size]); a rule
+// holds iff for every class it constrains the packet has the field and the
+// masked field equals the rule's value (two terms of one class with
+// different values, or an LD_VNI term, make it unmatchable -- not "alive").
+// Every class has a cuckoo table keyed by the values its rules require; a
+// packet's lookup (absent field = miss) selects:
+//  * DIRECT mode (one class): the first alive rule among "rules with this
+//    key or without a term of the class" (stored as 1 + rule); a miss takes
+//    the first alive rule without a term of the class.
+//  * BITMAP mode (<= 32 rules): the 32-bit row "rules with this key or
+//    without a term of the class"; a miss takes the row of the latter.  The
+//    AND of the rows with the alive row has the first holding rule as its
+//    lowest set bit.
+//  * CANDIDATE mode: every distinct (class, value) has a key id (1..); the
+//    lookup gives the packet's key id (0: miss).  Every constraining rule is
+//    filed under ONE of its classes -- its "primary", the one whose value
+//    the fewest rules share -- in a list per key id in scan order.  The
+//    candidates are the lists of the packet's key ids plus the first rule
+//    with no classified term (it matches everything); a candidate holds iff
+//    its record's key ids equal the packet's, and the smallest one wins.
 static bool build_bv(const mi_cos_t *cs, const mi_rule_t *rs, const mi_term_t *ts, uint32_t nrules,
 		     uint32_t base, std::vector<uint32_t> &blk)
 {
@@ -1574,22 +1692,20 @@ static bool build_bv(const mi_cos_t *cs, const mi_rule_t *rs, const mi_term_t *t
 			}
 		}
 	const uint32_t ncls = (uint32_t)cls_list.size();
-	if (ncls > BV_MAX_CLS)
+	if (ncls > BV_MAX_CLS || ncls == 0)
 		return false;
 	// canonical class order: CoS with the same classes evaluate them in the
 	// same order, so lanes on different CoS stay convergent
 	std::sort(cls_list.begin(), cls_list.end());
 	for (uint32_t i = 0; i < ncls; ++i)
 		cls[cls_list[i]] = i;
-	const uint32_t W = (nrules + 31u) / 32u;
-	// per rule: alive bit, and per class the required key (or none)
-	std::vector<uint32_t> alive(W, 0);
-	std::vector<std::map<Key4, std::vector<uint32_t>>> rows_of(ncls);   // key -> rule list
-	std::vector<std::vector<uint32_t>> dc(ncls, std::vector<uint32_t>(W, 0));
+	// per rule: alive, constrained classes and their values
+	std::vector<uint8_t> alive(nrules, 0);
+	std::vector<uint32_t> tmask(nrules, 0);
+	std::vector<std::vector<Key4>> want(nrules, std::vector<Key4>(ncls));
+	std::vector<std::map<Key4, uint32_t>> freq(ncls);   // value -> #alive rules
 	for (uint32_t r = 0; r < nrules; ++r) {
 		bool ok = true;
-		std::vector<int> have(ncls, 0);
-		std::vector<Key4> want(ncls);
 		for (uint32_t t = 0; t < rs[r].num_terms; ++t) {
 			const mi_term_t &tm = ts[rs[r].term_begin + t];
 			ClassKey ck;
@@ -1598,86 +1714,152 @@ static bool build_bv(const mi_cos_t *cs, const mi_rule_t *rs, const mi_term_t *t
 					ok = false;
 				continue;
 			}
-			uint32_t c = cls[ck];
+			const uint32_t c = cls[ck];
 			Key4 v = { 0, 0, 0, 0 };
 			for (uint32_t i = 0; i < ck.nkey; ++i)
 				v[i] = tm.value[i];
-			if (have[c] && want[c] != v)
+			if (((tmask[r] >> c) & 1u) && want[r][c] != v)
 				ok = false;   // two terms of one class with different values
-			have[c] = 1;
-			want[c] = v;
+			tmask[r] |= 1u << c;
+			want[r][c] = v;
 		}
 		if (!ok)
 			continue;
-		alive[r >> 5] |= 1u << (r & 31);
-		for (uint32_t c = 0; c < ncls; ++c) {
-			if (have[c])
-				rows_of[c][want[c]].push_back(r);
-			else
-				dc[c][r >> 5] |= 1u << (r & 31);
-		}
+		alive[r] = 1;
+		for (uint32_t c = 0; c < ncls; ++c)
+			if ((tmask[r] >> c) & 1u)
+				freq[c][want[r][c]]++;
 	}
-	// layout: header (4) | classes (16 each) | alive row | results |
-	//         per class: table [, rows]
-	const bool direct = ncls == 1;
-	blk.assign(4 + BV_CLS_WORDS * ncls, 0);
-	blk[0] = direct ? 0u : W;
+	const uint32_t mode = ncls == 1 ? 0u : (nrules <= 32 ? 2u : 1u);
+	std::vector<std::map<Key4, uint32_t>> kid(ncls);   // value -> key id (1..)
+	for (uint32_t c = 0; c < ncls; ++c) {
+		uint32_t id = 1;
+		for (auto &kv : freq[c])
+			kid[c][kv.first] = id++;
+		if (id > 4096u)
+			return false;
+	}
+	auto holds_class = [&](uint32_t r, uint32_t c, const Key4 *v) {
+		return !((tmask[r] >> c) & 1u) || (v && want[r][c] == *v);
+	};
+	uint32_t wc_first = BV_NONE;   // first alive rule without a classified term
+	for (uint32_t r = 0; r < nrules && wc_first == BV_NONE; ++r)
+		if (alive[r] && tmask[r] == 0u)
+			wc_first = r;
+	// header (8) | classes (16 each) | results | [records] | per class: table [, lists]
+	blk.assign(8 + BV_CLS_WORDS * ncls, 0);
+	blk[0] = mode;
 	blk[1] = ncls;
+	blk[3] = wc_first;
 	blk[2] = base + (uint32_t)blk.size();
-	blk.insert(blk.end(), alive.begin(), alive.end());
-	blk[3] = base + (uint32_t)blk.size();
 	for (uint32_t r = 0; r < nrules; ++r)
 		blk.push_back((rs[r].dst_cos & 0xffu) | (cs[rs[r].dst_cos].num_rules == 0 ? 0x100u : 0u) |
 			      ((uint32_t)rs[r].mark << 16));
-	auto first_live = [&](const std::vector<uint32_t> &bits) -> uint32_t {
-		for (uint32_t i = 0; i < W; ++i)
-			if (bits[i] & alive[i])
-				return i * 32u + (uint32_t)__builtin_ctz(bits[i] & alive[i]);
+	std::vector<std::vector<std::vector<uint32_t>>> lists(ncls);   // [class][key id] -> rules
+	if (mode == 2u) {
+		uint32_t aw = 0;
+		for (uint32_t r = 0; r < nrules; ++r)
+			aw |= (uint32_t)alive[r] << r;
+		blk[4] = aw;
+	} else if (mode == 1u) {
+		const uint32_t RW = 1u + (ncls + 1u) / 2u;
+		blk[4] = base + (uint32_t)blk.size();
+		blk[5] = RW;
+		for (uint32_t c = 0; c < ncls; ++c)
+			lists[c].resize(kid[c].size() + 1);
+		for (uint32_t r = 0; r < nrules; ++r) {
+			std::vector<uint32_t> rec(RW, 0);
+			if (alive[r]) {
+				rec[0] = tmask[r];
+				uint32_t prim = BV_NONE, best = 0xFFFFFFFFu;
+				for (uint32_t c = 0; c < ncls; ++c) {
+					if (!((tmask[r] >> c) & 1u))
+						continue;
+					rec[1 + c / 2] |= kid[c][want[r][c]] << (16 * (c & 1u));
+					const uint32_t f = freq[c][want[r][c]];
+					if (f < best) {
+						best = f;
+						prim = c;
+					}
+				}
+				if (prim != BV_NONE)
+					lists[prim][kid[prim][want[r][prim]]].push_back(r);
+			} else {
+				rec[0] = 0x80000000u;   // never holds
+			}
+			blk.insert(blk.end(), rec.begin(), rec.end());
+		}
+	}
+	auto first_live = [&](uint32_t c, const Key4 *v) -> uint32_t {
+		for (uint32_t r = 0; r < nrules; ++r)
+			if (alive[r] && holds_class(r, c, v))
+				return r;
 		return BV_NONE;
+	};
+	auto row_of = [&](uint32_t c, const Key4 *v) -> uint32_t {
+		uint32_t w = 0;
+		for (uint32_t r = 0; r < nrules; ++r)
+			if (holds_class(r, c, v))
+				w |= 1u << r;
+		return w;
 	};
 	for (uint32_t c = 0; c < ncls; ++c) {
 		const ClassKey &ck = cls_list[c];
-		const uint32_t nvals = (uint32_t)rows_of[c].size();
-		uint32_t tsize = 4;
-		while (tsize < 2 * (nvals + 1))
-			tsize <<= 1;
-		const uint32_t cbase = 4 + BV_CLS_WORDS * c;
+		std::vector<Key4> keys;
+		for (auto &kv : kid[c])
+			keys.push_back(kv.first);
+		uint32_t nb = 4, m1 = 1, m2 = 3;
+		std::vector<uint32_t> slot_of;
+		if (!cuckoo_place(keys, nb, m1, m2, slot_of))
+			return false;
+		const uint32_t cbase = 8 + BV_CLS_WORDS * c;
+		const uint32_t SW = ck.nkey + 1u;   // slot: key words, value
 		blk[cbase + 0] = ck.kind;
 		blk[cbase + 1] = ck.nkey;
-		blk[cbase + 2] = direct ? first_live(dc[c]) : 0u;
+		blk[cbase + 2] = mode == 0u ? first_live(c, nullptr) : (mode == 2u ? row_of(c, nullptr) : 0u);
 		blk[cbase + 3] = ck.offset;
 		blk[cbase + 4] = ck.size;
 		for (int i = 0; i < 4; ++i)
 			blk[cbase + 5 + i] = ck.mask[i];
-		blk[cbase + 9] = tsize - 1;
+		blk[cbase + 9] = nb;
+		blk[cbase + 11] = m1;
+		blk[cbase + 12] = m2;
 		const uint32_t tbl_off = (uint32_t)blk.size();
-		blk.resize(blk.size() + (size_t)tsize * (ck.nkey + 1), 0);
-		for (uint32_t i = 0; i < tsize; ++i)
-			blk[tbl_off + i * (ck.nkey + 1) + ck.nkey] = BV_EMPTY;
-		const uint32_t rows_off = (uint32_t)blk.size();
-		if (!direct)   // row 0: rules without a term of this class
-			blk.insert(blk.end(), dc[c].begin(), dc[c].end());
-		uint32_t row = 1;
-		for (auto &kv : rows_of[c]) {
-			std::vector<uint32_t> bits = dc[c];
-			for (uint32_t r : kv.second)
-				bits[r >> 5] |= 1u << (r & 31);
-			uint32_t val;
-			if (direct) {
-				val = first_live(bits);
-			} else {
-				blk.insert(blk.end(), bits.begin(), bits.end());
-				val = row++;
-			}
-			uint32_t h = host_bv_hash(kv.first) & (tsize - 1);
-			while (blk[tbl_off + h * (ck.nkey + 1) + ck.nkey] != BV_EMPTY)
-				h = (h + 1) & (tsize - 1);
-			for (uint32_t i = 0; i < ck.nkey; ++i)
-				blk[tbl_off + h * (ck.nkey + 1) + i] = kv.first[i];
-			blk[tbl_off + h * (ck.nkey + 1) + ck.nkey] = val;
-		}
 		blk[cbase + 10] = base + tbl_off;
-		blk[cbase + 11] = base + rows_off;
+		// empty slots keep key words 0 and value 0: a miss (every stored
+		// value is non-zero)
+		blk.resize(blk.size() + (size_t)nb * SW, 0);
+		uint32_t list_at = 0;
+		if (mode == 1u) {
+			blk[cbase + 13] = base + (uint32_t)blk.size();
+			for (auto &l : lists[c]) {
+				if (l.size() > 255u)
+					return false;   // degenerate: the linear scan is cheaper
+				blk.insert(blk.end(), l.begin(), l.end());
+			}
+			if (blk.size() - (blk[cbase + 13] - base) > 4095u)
+				return false;
+		}
+		for (uint32_t i = 0; i < keys.size(); ++i) {
+			const uint32_t sl = tbl_off + slot_of[i] * SW;
+			for (uint32_t j = 0; j < ck.nkey; ++j)
+				blk[sl + j] = keys[i][j];
+			uint32_t val;
+			if (mode == 0u) {
+				const uint32_t f = first_live(c, &keys[i]);
+				val = f == BV_NONE ? BV_EMPTY : f + 1u;
+			} else if (mode == 2u) {
+				val = row_of(c, &keys[i]);   // non-zero: the key's own rules
+			} else {
+				const uint32_t id = kid[c][keys[i]];
+				uint32_t off = 0;
+				for (uint32_t q = 0; q < id; ++q)
+					off += (uint32_t)lists[c][q].size();
+				val = id | ((uint32_t)lists[c][id].size() << 12) | (off << 20);
+			}
+			blk[sl + ck.nkey] = val;
+		}
+		(void)list_at;
 	}
 	return true;
 }

@@ -1,8 +1,8 @@
 #!/bin/bash
 # A/B kernel variants on the GPU box: build each -D set into its own dir and
-# time the bench's kernel for several workloads.  An argument starting with
-# "env " runs the in-tree build with those environment settings instead.
-#   tools/variants.sh "WIN=128" "WIN=64 MIN_WAVES_PER_EU=2" "env MI_CLS_LDS_HOT_MAX=0"
+# time the bench's kernel for several workloads.  "DEFS|ENV" runs the build
+# with -D DEFS under environment ENV; "env ENV" uses the in-tree build.
+#   tools/variants.sh "WIN=128" "WIN=96 WAVES_PER_BLOCK=16|MI_CLS_LDS_HOT_MAX=52000"
 set -o pipefail
 CFGS=${CFGS:-"20 2 3 5"}
 mkdir -p gpurun_out
@@ -10,11 +10,14 @@ i=0
 for v in "$@"; do
   d=$(pwd)/odp_amd
   envs=""
+  defs=""
   if [[ "$v" == env\ * ]]; then
     envs=${v#env }
   else
+    defs=${v%%|*}
+    [[ "$v" == *"|"* ]] && envs=${v#*|}
     d=/tmp/variant_$i
-    timeout -k 10 300 python -m odp_amd._build $d $v > /dev/null || exit 1
+    timeout -k 10 300 python -m odp_amd._build $d $defs > /dev/null || exit 1
   fi
   for c in $CFGS; do
     env $envs ODP_AMD_LIB_DIR=$d timeout -k 10 200 python bench.py --config $c --steps 30 --warmup 5 \
