@@ -40,12 +40,8 @@
 #include <vector>
 
 #define WAVE 64
-#ifndef WAVES_PER_BLOCK
-#define WAVES_PER_BLOCK 4
-#endif
-#define BLOCK (WAVE * WAVES_PER_BLOCK)
 #ifndef WIN
-#define WIN 128            // staged header window, bytes (multiple of 16)
+#define WIN 96             // staged header window, bytes (96 or 128)
 #endif
 #define WROWS (WIN / 4 + 1)     // LDS dword rows per wave window (+1 zero row)
 #define RS 66                   // LDS row stride of a window, dwords (see load_window)
@@ -1108,10 +1104,13 @@ __device__ __forceinline__ void wave_lds_sync()
 // region from HBM (large rule sets).
 extern __shared__ uint32_t s_dyn[];
 
-template <bool LT, bool DIV>
-__global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_EU) void mi_cls_kernel(KArgs a)
+// NW = waves per block: 4 (each block copies the hot region for itself), or
+// 16 = one block per CU whose 16 waves share one LDS copy of a larger hot
+// region.  Either way 4 waves per SIMD (the VGPR budget).
+template <bool LT, bool DIV, int NW>
+__global__ __launch_bounds__(NW * WAVE, MIN_WAVES_PER_EU) void mi_cls_kernel(KArgs a)
 {
-	__shared__ uint32_t s_win[WAVES_PER_BLOCK * RS * WROWS];
+	__shared__ uint32_t s_win[NW * RS * WROWS];
 	__shared__ uint32_t s_cnt[MAX_STATS_COS];
 
 	const uint32_t lane = threadIdx.x & (WAVE - 1);
@@ -1129,10 +1128,26 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_EU) void mi_cls_kernel(KArgs a
 	const bool stats_on = a.stats != nullptr;
 	typedef typename std::conditional<LT, lword_t, gword_t>::type hot_t;
 	hot_t H;
+	// first descriptors before the hot-region copy: their latency overlaps it
+	const uint32_t nt = (a.n + WAVE - 1) / WAVE;
+	const uint32_t tstride = gridDim.x * NW;
+	uint32_t tile = blockIdx.x * NW + wave;
+	uint32_t d_off = 0, d_len = 0, n_off = 0, n_len = 0;
+	{
+		const uint32_t p0 = tile * WAVE + lane, p1 = (tile + tstride) * WAVE + lane;
+		if (tile < nt && p0 < a.n) {
+			d_off = a.off[p0];
+			d_len = a.len[p0];
+		}
+		if (tile + tstride < nt && p1 < a.n) {
+			n_off = a.off[p1];
+			n_len = a.len[p1];
+		}
+	}
 	if constexpr (LT) {
 		const uint32_t hw = dev[DH_HOT_WORDS];
 		const gword_t src = (gword_t)(a.dev + hot_off);
-		for (uint32_t i = threadIdx.x; i < hw; i += BLOCK)
+		for (uint32_t i = threadIdx.x; i < hw; i += NW * WAVE)
 			s_dyn[i] = src[i];
 		H = (lword_t)s_dyn;
 	} else {
@@ -1140,7 +1155,7 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_EU) void mi_cls_kernel(KArgs a
 	}
 
 	if (stats_on) {
-		for (uint32_t i = threadIdx.x; i < MAX_STATS_COS; i += BLOCK)
+		for (uint32_t i = threadIdx.x; i < MAX_STATS_COS; i += NW * WAVE)
 			s_cnt[i] = 0;
 	}
 	if (LT || stats_on)
@@ -1155,28 +1170,13 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_EU) void mi_cls_kernel(KArgs a
 	// records are not held in registers through parse and classify.
 	const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
 		(void *)a.pkts, (short)0, (int)OOB_OFF, 0x00020000);
-	const uint32_t nt = (a.n + WAVE - 1) / WAVE;
-	const uint32_t tstride = gridDim.x * WAVES_PER_BLOCK;
-	uint32_t tile = blockIdx.x * WAVES_PER_BLOCK + wave;
-	uint32_t d_off = 0, d_len = 0, n_off = 0, n_len = 0;
 	u32x4 d[NPIECE];
 	bool d_hi, hi_rows = true;
 	W[(WIN / 4) * RS + lane] = 0u;   // pad row: always zero
 	uint4 prev_rec = make_uint4(0, 0, 0, 0);
 	uint32_t prev_pi = 0;
 	bool prev_valid = false;
-	{
-		const uint32_t p0 = tile * WAVE + lane, p1 = (tile + tstride) * WAVE + lane;
-		if (tile < nt && p0 < a.n) {
-			d_off = a.off[p0];
-			d_len = a.len[p0];
-		}
-		if (tile + tstride < nt && p1 < a.n) {
-			n_off = a.off[p1];
-			n_len = a.len[p1];
-		}
-		d_hi = load_window(rs, d_off, d_len, lane, d);
-	}
+	d_hi = load_window(rs, d_off, d_len, lane, d);
 #ifdef DIAG_STAMPS
 	unsigned long long st_acc[NSTAMP] = { 0 }, st_last;
 	asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_last) :: "memory");
@@ -1184,7 +1184,7 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_EU) void mi_cls_kernel(KArgs a
 	for (; tile < nt; tile += tstride) {
 		const uint32_t pi = tile * WAVE + lane;
 		const bool valid = pi < a.n;
-		if (!PREFETCH && tile != blockIdx.x * WAVES_PER_BLOCK + wave) {
+		if (!PREFETCH && tile != blockIdx.x * NW + wave) {
 			d_off = valid ? a.off[pi] : 0u;
 			d_len = valid ? (uint32_t)a.len[pi] : 0u;
 			d_hi = load_window(rs, d_off, d_len, lane, d);
@@ -1371,7 +1371,7 @@ __global__ __launch_bounds__(BLOCK, MIN_WAVES_PER_EU) void mi_cls_kernel(KArgs a
 
 	if (stats_on) {
 		__syncthreads();
-		for (uint32_t i = threadIdx.x; i < MAX_STATS_COS; i += BLOCK)
+		for (uint32_t i = threadIdx.x; i < MAX_STATS_COS; i += NW * WAVE)
 			if (s_cnt[i])
 				atomicAdd(a.stats + i, (unsigned long long)s_cnt[i]);
 	}
@@ -1385,6 +1385,7 @@ struct mi_cls_ctx {
 	int loaded;
 	uint32_t hot_words;      // size of the program's hot region
 	int tree;                // some rule leads to a CoS with rules (DIV kernel)
+	int wpb;                 // forced waves per block (MI_CLS_WPB at load), 0 = auto
 	unsigned long long *d_stats;
 	int stats_on;
 	uint32_t stats_mask[8];
@@ -1972,6 +1973,8 @@ extern "C" int mi_cls_rules_load(mi_cls_ctx_t *c, const void *tbl, size_t bytes,
 		const char *e = getenv("MI_CLS_DIV");
 		if (e)
 			tree = atoi(e) != 0;
+		e = getenv("MI_CLS_WPB");
+		c->wpb = e ? atoi(e) : 0;
 	}
 	if (getenv("MI_CLS_VERBOSE"))
 		fprintf(stderr, "mi_cls: program %zu words, hot region %u words\n", words, hot_words);
@@ -2047,34 +2050,63 @@ extern "C" int mi_cls_classify(mi_cls_ctx_t *c, const uint8_t *pkts, const uint3
 		e = getenv("MI_CLS_LDS_HOT_MAX");
 		hot_max = e ? atoi(e) : 20 * 1024;
 	}
+	// Block shape: 4-wave blocks, each with its own LDS copy of the hot
+	// region when it is small (<= MI_CLS_LDS_HOT_MAX); one 16-wave block per
+	// CU sharing a copy when it fits the LDS left beside 16 windows; else
+	// 4-wave blocks reading the hot region from HBM.  MI_CLS_WPB=4|16
+	// forces a shape (A/B runs).
+	const int wpb_env = c->wpb;
+	const size_t LDS_CU = 160u * 1024u;
 	const size_t hot_bytes = (size_t)c->hot_words * sizeof(uint32_t);
-	const bool lt = (long)hot_bytes <= (long)hot_max;
-	const size_t lds_static = sizeof(uint32_t) * (WAVES_PER_BLOCK * RS * WROWS + MAX_STATS_COS);
-	const size_t lds_block = lds_static + (lt ? hot_bytes : 0);
+	const size_t st4 = sizeof(uint32_t) * (4 * RS * WROWS + MAX_STATS_COS);
+	const size_t st16 = sizeof(uint32_t) * (16 * RS * WROWS + MAX_STATS_COS);
+	const bool fits16 = st16 + hot_bytes <= LDS_CU;
+	bool lt = (long)hot_bytes <= (long)hot_max;
+	// 4-wave blocks reach 4 blocks (16 waves) per CU only while four LDS
+	// copies of the hot region fit; past that one shared copy keeps 16 waves
+	const bool full4 = lt && 4 * (st4 + hot_bytes) <= LDS_CU;
+	int nw = (!full4 && fits16) ? 16 : 4;
+	if (wpb_env == 4 || wpb_env == 16)
+		nw = wpb_env;
+	lt = nw == 16 ? fits16 : lt;
+	const size_t lds_block = (nw == 16 ? st16 : st4) + (lt ? hot_bytes : 0);
 	const bool div = c->tree;
-	int per_cu = (int)((160u * 1024u) / lds_block);
+	int per_cu = (int)(LDS_CU / lds_block);
 	const int occ = MIN_WAVES_PER_EU;   // waves/SIMD the register budget allows
-	if (per_cu > occ * 4 / WAVES_PER_BLOCK)
-		per_cu = occ * 4 / WAVES_PER_BLOCK;
+	if (per_cu > occ * 4 / nw)
+		per_cu = occ * 4 / nw;
 	if (per_cu_env > 0)
 		per_cu = per_cu_env;
 	if (per_cu < 1)
 		per_cu = 1;
-	uint32_t tiles = (n + BLOCK - 1) / BLOCK;
+	const uint32_t bthreads = (uint32_t)nw * WAVE;
+	uint32_t tiles = (n + bthreads - 1) / bthreads;
 	uint32_t max_grid = (uint32_t)c->num_cu * (uint32_t)per_cu;
 	uint32_t grid = tiles < max_grid ? tiles : max_grid;
-	if (lt && div)
-		hipLaunchKernelGGL((mi_cls_kernel<true, true>), dim3(grid), dim3(BLOCK), hot_bytes,
-				   (hipStream_t)stream, a);
-	else if (lt)
-		hipLaunchKernelGGL((mi_cls_kernel<true, false>), dim3(grid), dim3(BLOCK), hot_bytes,
-				   (hipStream_t)stream, a);
-	else if (div)
-		hipLaunchKernelGGL((mi_cls_kernel<false, true>), dim3(grid), dim3(BLOCK), 0,
-				   (hipStream_t)stream, a);
-	else
-		hipLaunchKernelGGL((mi_cls_kernel<false, false>), dim3(grid), dim3(BLOCK), 0,
-				   (hipStream_t)stream, a);
+	const size_t dyn = lt ? hot_bytes : 0;
+	hipStream_t st = (hipStream_t)stream;
+#define MI_LAUNCH(L_, D_, N_) \
+	hipLaunchKernelGGL((mi_cls_kernel<L_, D_, N_>), dim3(grid), dim3(N_ * WAVE), dyn, st, a)
+	if (nw == 16) {
+		if (lt && div)
+			MI_LAUNCH(true, true, 16);
+		else if (lt)
+			MI_LAUNCH(true, false, 16);
+		else if (div)
+			MI_LAUNCH(false, true, 16);
+		else
+			MI_LAUNCH(false, false, 16);
+	} else {
+		if (lt && div)
+			MI_LAUNCH(true, true, 4);
+		else if (lt)
+			MI_LAUNCH(true, false, 4);
+		else if (div)
+			MI_LAUNCH(false, true, 4);
+		else
+			MI_LAUNCH(false, false, 4);
+	}
+#undef MI_LAUNCH
 	if (hipGetLastError() != hipSuccess)
 		return -EIO;
 #ifdef DIAG_STAMPS

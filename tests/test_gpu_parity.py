@@ -21,6 +21,8 @@ ENGINE_ENV = {
     "linear": {"MI_CLS_NO_BV": "1"},   # linear scan everywhere
     "nodiv": {"MI_CLS_DIV": "0"},      # no per-lane bit-vector rounds (CoS waterfall)
     "div": {"MI_CLS_DIV": "1"},        # per-lane bit-vector rounds even for flat programs
+    "wpb4": {"MI_CLS_WPB": "4"},       # 4-wave blocks (own hot-region copy or HBM)
+    "wpb16": {"MI_CLS_WPB": "16"},     # one 16-wave block per CU sharing the LDS copy
 }
 
 
@@ -29,7 +31,7 @@ def both(prog, batch, limits=(255, 8192, 4096), what="", engine="auto"):
     linear scan otherwise, per-lane rounds for CoS trees; the other engines
     force one of the kernel's paths (ENGINE_ENV)."""
     import os
-    keys = ("MI_CLS_NO_BV", "MI_CLS_DIV")
+    keys = ("MI_CLS_NO_BV", "MI_CLS_DIV", "MI_CLS_WPB")
     old = {k: os.environ.pop(k, None) for k in keys}
     os.environ.update(ENGINE_ENV[engine])
     try:
@@ -92,7 +94,7 @@ def test_zoo_no_default(built, gpu):
     assert s["discard"] > 0 and s["cos_drop"] > 0
 
 
-@pytest.mark.parametrize("engine", ["auto", "linear", "nodiv", "div"])
+@pytest.mark.parametrize("engine", ["auto", "linear", "nodiv", "div", "wpb16"])
 @pytest.mark.parametrize("seed", range(12))
 def test_random_programs_fuzz(built, gpu, seed, engine):
     rng = np.random.default_rng(1000 + seed)
@@ -105,7 +107,7 @@ def test_random_programs_fuzz(built, gpu, seed, engine):
     both(prog, b, what=f"fuzz seed {seed}", engine=engine)
 
 
-@pytest.mark.parametrize("engine", ["auto", "linear", "nodiv"])
+@pytest.mark.parametrize("engine", ["auto", "linear", "nodiv", "wpb4", "wpb16"])
 @pytest.mark.parametrize("cfg,n", [(1, 10_000), (2, 100_000), (3, 50_000), (4, 50_000),
                                    (5, 20_000)])
 def test_configs_small(built, gpu, cfg, n, engine):
