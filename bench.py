@@ -12,9 +12,13 @@ its own 1 M-packet shard (weak scaling, no data-path collective); the timed
 region is bracketed by barrier + synchronize and the max over ranks is taken.
 
 Extra fields on the JSON line:
-  roofline      HBM roofline of the dominant kernel, from HIP events on the
-                launch stream (algorithmic bytes: min(len,128) + 6 B
-                descriptor + 16 B result per packet)
+  roofline      HBM roofline of the dominant kernel: algorithmic bytes
+                (min(len,128) + 6 B descriptor + 16 B result per packet) over
+                the average launch duration, from HIP events on the launch
+                stream in a second, single-stream pass (launches back to back,
+                no overlap, so it agrees with rocprofv3's per-dispatch
+                average); `pipelined_*` are the same bytes over the
+                per-step time of the two-stream `value` pass
   cpu_baseline  the oracle (scalar C restatement, 1 thread) timed on this
                 host over repeated passes of the same batch
   e2e           end-to-end rate including pinned H2D of the batch and D2H of
@@ -44,6 +48,9 @@ def parse_args():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-extra", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="HIP streams the consecutive batches alternate over (the timed "
+                         "`value` pass); the roofline pass always uses one stream")
     ap.add_argument("--rotate", type=int, default=4,
                     help="distinct device copies of the batch, used round-robin, so the "
                          "working set (R x batch) exceeds the 256 MiB Infinity Cache and every "
@@ -83,7 +90,7 @@ def to_device(batch, dev):
     return t_buf, t_off, t_len, t_out
 
 
-def time_device(c, batch, dev, steps, warmup, dist_on=False, rotate=1):
+def time_device(c, batch, dev, steps, warmup, dist_on=False, rotate=1, streams=1):
     """Warmup, then time `steps` launches; returns (wall_s, avg_kernel_ms, out tensor).
     With rotate > 1 the launches cycle over that many device copies of the
     batch (and of the result array), so consecutive steps do not re-read
@@ -95,29 +102,44 @@ def time_device(c, batch, dev, steps, warmup, dist_on=False, rotate=1):
         b0 = copies[0]
         copies.append(tuple(t.clone() for t in b0[:3]) + (torch.empty_like(b0[3]),))
     stream = torch.cuda.current_stream(dev)
-    sp = stream.cuda_stream
-    arglist = [(cb.data_ptr(), co.data_ptr(), cl.data_ptr(), batch.n, cout.data_ptr(), sp)
-               for cb, co, cl, cout in copies]
+    # streams > 1: consecutive batches alternate between streams, so one
+    # launch's ramp-up overlaps the previous one's tail (a pipelined receive
+    # path keeps several bursts in flight the same way); copy i always runs on
+    # stream i % streams, so no two in-flight launches share buffers
+    strm = [stream] + [torch.cuda.Stream(dev) for _ in range(1, max(1, streams))]
+    if len(copies) % len(strm):
+        raise ValueError("rotate must be a multiple of streams")
+    arglist = [(cb.data_ptr(), co.data_ptr(), cl.data_ptr(), batch.n, cout.data_ptr(),
+                strm[i % len(strm)].cuda_stream)
+               for i, (cb, co, cl, cout) in enumerate(copies)]
     t_out = copies[0][3]
     for i in range(warmup):
         rc = c.classify_device(*arglist[i % len(arglist)])
         assert rc == 0, rc
     torch.cuda.synchronize(dev)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(steps)]
+    # HIP events on the launch stream bracket the timed region (no per-launch
+    # events inside it: each record is a host call between launches); the
+    # average launch duration is their span / steps (kernels + the gaps
+    # between back-to-back launches)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
     if dist_on:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    ev0.record(stream)
+    for s_ in strm[1:]:
+        s_.wait_event(ev0)
     for i in range(steps):
-        ev[i][0].record(stream)
         c.classify_device(*arglist[i % len(arglist)])
-        ev[i][1].record(stream)
+    for s_ in strm[1:]:
+        stream.wait_stream(s_)
+    ev1.record(stream)
     torch.cuda.synchronize(dev)
     if dist_on:
         dist.barrier()
     wall = time.perf_counter() - t0
-    kms = sum(a.elapsed_time(b) for a, b in ev) / steps
+    kms = ev0.elapsed_time(ev1) / steps
     return wall, kms, t_out
 
 
@@ -219,7 +241,12 @@ def main():
     c = cls.Classifier(gpu=local)
     c.apply(prog)
 
-    wall, kms, t_out = time_device(c, batch, dev, a.steps, a.warmup, dist_on, a.rotate)
+    wall, kms_pipe, t_out = time_device(c, batch, dev, a.steps, a.warmup, dist_on, a.rotate,
+                                        a.streams)
+    if a.streams > 1:
+        _, kms, _ = time_device(c, batch, dev, a.steps, a.warmup, dist_on, a.rotate, 1)
+    else:
+        kms = kms_pipe
     if dist_on:
         t = torch.tensor([wall], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -228,6 +255,7 @@ def main():
     value = total_pkts / wall / 1e6
     bytes_launch = batch.header_bytes()
     achieved = bytes_launch / (kms * 1e-3) / 1e9
+    achieved_pipe = bytes_launch / (kms_pipe * 1e-3) / 1e9
     res = None
     if rank == 0:
         out = t_out.cpu().numpy().view(np.uint8).reshape(-1)[: 16 * batch.n].view(R.RESULT_DTYPE)
@@ -252,7 +280,10 @@ def main():
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": load_traffic(a.config, batch.n),
                          "kernel": "mi_cls_kernel", "kernel_ms": round(kms, 5),
-                         "bytes_per_launch": bytes_launch},
+                         "bytes_per_launch": bytes_launch,
+                         "pipelined_achieved": round(achieved_pipe, 2),
+                         "pipelined_frac": round(achieved_pipe / HBM_PEAK_GBS, 5),
+                         "streams": a.streams},
         }
         if world == 1:
             try:
@@ -272,7 +303,9 @@ def main():
                     c2 = cls.Classifier(gpu=local)
                     c2.apply(p2)
                     k_steps = max(5, a.steps // 5)
-                    w2, k2, _ = time_device(c2, b2, dev, k_steps, 3, rotate=a.rotate)
+                    w2, _, _ = time_device(c2, b2, dev, k_steps, 3, rotate=a.rotate,
+                                           streams=a.streams)
+                    _, k2, _ = time_device(c2, b2, dev, k_steps, 3, rotate=a.rotate)
                     c2.close()
                     ach = b2.header_bytes() / (k2 * 1e-3) / 1e9
                     extra[names[cfg]] = {

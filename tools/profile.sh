@@ -14,7 +14,7 @@ cd /tmp
 export TMPDIR=/tmp
 ARGS=("$@")
 if [ ${#ARGS[@]} -eq 0 ]; then
-  ARGS=(--steps 20 --warmup 5 --no-cpu --no-extra)
+  ARGS=(--steps 20 --warmup 5 --no-cpu --no-extra --streams 1)
 fi
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o kt \
   -- python3 "$ROOT/bench.py" "${ARGS[@]}" > "$OUT/kt.log" 2>&1
