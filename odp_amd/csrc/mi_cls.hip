@@ -330,52 +330,86 @@ __device__ __forceinline__ uint32_t bsw16(uint32_t v)   // be16 of the low half
 	return ((v & 0xffu) << 8) | ((v >> 8) & 0xffu);
 }
 
-// Branch-free parse of the common frame shapes: DIX or SNAP, 0-2 VLAN tags,
+// L4 protocol table (one LDS word per IP protocol number, copied in at block
+// start): the F_L4 / kind flags _odp_packet_parse_common_l3_l4 sets for the
+// protocol (odp_parse.c:395-460) in bits 0..26, and in bits 28..29 the L4
+// header check the protocol takes (1 TCP, 2 UDP, 3 SCTP).  Protocol 255 is
+// "no IP" and 0 a bad IP header: neither sets anything.
+#define L4K_TCP 1u
+#define L4K_UDP 2u
+#define L4K_SCTP 3u
+struct L4Tab {
+	uint32_t v[256];
+	constexpr L4Tab() : v()
+	{
+		v[1] = v[58] = F_L4 | F_ICMP;
+		v[4] = F_L4;
+		v[6] = F_L4 | F_TCP | (L4K_TCP << 28);
+		v[17] = F_L4 | F_UDP | (L4K_UDP << 28);
+		v[51] = F_L4 | F_IPSEC | F_AH;
+		v[50] = F_L4 | F_IPSEC | F_ESP;
+		v[132] = F_L4 | F_SCTP | (L4K_SCTP << 28);
+		v[59] = F_L4 | F_NO_NEXT;
+	}
+};
+__constant__ L4Tab c_l4tab;
+
+// Branch-light parse of the common frame shapes: DIX or SNAP, 0-2 VLAN tags,
 // IPv4 (any IHL / errors), IPv6 without HBH / routing headers, ARP, every L4.
 // The reference places L3 at 14/18/22/26/30, so every L3 and L4 offset here is
 // 2 (mod 4) and all header words are one alignbyte of two window dwords.
-// Written as selects (no data-dependent branches) so the wave runs it with a
-// full exec mask; lanes it cannot finish (IPv6 extension chain, L4 header
-// past the window) set `slow` and are re-parsed by parse_packet.  Results are
-// identical to parse_packet for every lane that does not set `slow`.
-__device__ __forceinline__ Parsed parse_fast(const Pkt &k, bool &slow)
+// Per lane it is written as selects (no data-dependent lane branches); the
+// only branches are wave-uniform ones that skip a header family no lane of
+// the tile has (tags / SNAP, IPv4, IPv6, TCP-UDP-SCTP checks), so a tile of
+// untagged IPv4 frames runs just the IPv4 and its L4 code.  Lanes it cannot
+// finish (IPv6 extension chain, L4 header past the window) set `slow` and are
+// re-parsed by parse_packet.  Results are identical to parse_packet for every
+// lane that does not set `slow`.
+__device__ __forceinline__ Parsed parse_fast(const Pkt &k, const uint32_t *l4tab, bool &slow)
 {
 	Parsed r;
 	const uint32_t len = k.len;
-	uint32_t w[8];
-#pragma unroll
-	for (int i = 0; i < 8; ++i) {
-		w[i] = k.w[i * RS];
-		// opaque register value: keeps the selects below v_cndmask instead of
-		// letting the compiler fold them into an indexed (scratch) load of w[]
-		asm("" : "+v"(w[i]));
-	}
+	const uint32_t w0 = k.w[0], w1 = k.w[RS], w3 = k.w[3 * RS];
 
 	uint32_t f = F_L2 | F_ETH;
 	f |= len > 1514u ? F_JUMBO : 0u;
-	f |= (w[0] & 1u) ? F_ETH_MCAST : 0u;
-	f |= (w[0] == 0xffffffffu && (w[1] & 0xffffu) == 0xffffu) ? F_ETH_BCAST : 0u;
-	const uint32_t et0 = bsw16(w[3]);
-	const bool snap = et0 < 1514u;
-	const bool snap_err = snap && et0 > len - 14u;
-	uint32_t e = snap ? bsw16(w[5]) : et0;
-	uint32_t off = snap ? 22u : 14u;
-	// outer tag: type at off+2 = 16 / 24
-	const bool qinq = e == 0x88A8u;
-	e = qinq ? bsw16(snap ? w[6] : w[4]) : e;
-	off += qinq ? 4u : 0u;
-	// inner tag: type at off+2 = 16 / 20 / 24 / 28 (off = 14 + 8 snap + 4 qinq);
-	// selected by the two booleans, not by an index (an index would make the
-	// compiler spill w[] to scratch)
-	const bool vlan = e == 0x8100u;
-	const uint32_t wv = snap ? (qinq ? w[7] : w[6]) : (qinq ? w[5] : w[4]);
-	e = vlan ? bsw16(wv) : e;
-	off += vlan ? 4u : 0u;
-	uint32_t err = snap_err ? E_SNAP : 0u;
-	e = snap_err ? 0u : e;
-	off = snap_err ? 14u : off;
-	f |= (!snap_err && qinq) ? (F_QINQ | F_VLAN) : 0u;
-	f |= (!snap_err && vlan) ? F_VLAN : 0u;
+	f |= (w0 & 1u) << 8;   // F_ETH_MCAST
+	f |= (w0 == 0xffffffffu && (w1 & 0xffffu) == 0xffffu) ? F_ETH_BCAST : 0u;
+	const uint32_t et0 = bsw16(w3);
+	uint32_t e = et0, off = 14u, err = 0u;
+	bool snap_err = false;
+	if (__ballot(et0 < 1514u || et0 == 0x88A8u || et0 == 0x8100u) != 0ull) {
+		// some lane has SNAP or a tag
+		uint32_t w[8];
+#pragma unroll
+		for (int i = 0; i < 8; ++i) {
+			w[i] = k.w[i * RS];
+			// opaque register value: keeps the selects below v_cndmask
+			// instead of letting the compiler fold them into an indexed
+			// (scratch) load of w[]
+			asm("" : "+v"(w[i]));
+		}
+		const bool snap = et0 < 1514u;
+		snap_err = snap && et0 > len - 14u;
+		e = snap ? bsw16(w[5]) : et0;
+		off = snap ? 22u : 14u;
+		// outer tag: type at off+2 = 16 / 24
+		const bool qinq = e == 0x88A8u;
+		e = qinq ? bsw16(snap ? w[6] : w[4]) : e;
+		off += qinq ? 4u : 0u;
+		// inner tag: type at off+2 = 16 / 20 / 24 / 28 (off = 14 + 8 snap +
+		// 4 qinq); selected by the two booleans, not by an index (an index
+		// would make the compiler spill w[] to scratch)
+		const bool vlan = e == 0x8100u;
+		const uint32_t wv = snap ? (qinq ? w[7] : w[6]) : (qinq ? w[5] : w[4]);
+		e = vlan ? bsw16(wv) : e;
+		off += vlan ? 4u : 0u;
+		err = snap_err ? E_SNAP : 0u;
+		e = snap_err ? 0u : e;
+		off = snap_err ? 14u : off;
+		f |= (!snap_err && qinq) ? (F_QINQ | F_VLAN) : 0u;
+		f |= (!snap_err && vlan) ? F_VLAN : 0u;
+	}
 	const bool short_l2 = !snap_err && off > len;
 	f = short_l2 ? F_L2 : f;
 	e = short_l2 ? 0u : e;
@@ -395,77 +429,84 @@ __device__ __forceinline__ Parsed parse_fast(const Pkt &k, bool &slow)
 	const bool is4 = e == 0x0800u, is6 = e == 0x86DDu, isarp = e == 0x0806u;
 	f |= (is4 || is6 || isarp) ? F_L3 : 0u;
 	f |= isarp ? F_ARP : 0u;
-	// IPv4 (parse_ipv4, odp_parse.c:112-167)
-	const uint32_t vi = hb[0] & 0xffu, ihl = vi & 0xfu;
-	const uint32_t tot = bsw16(hb[0] >> 16);
-	const bool bad4 = ihl < 5u || (vi >> 4) != 4u || 20u > len - l3 || tot > len - l3;
-	const uint32_t frag = bsw16(hb[1] >> 16);
-	const uint32_t dst = __builtin_bswap32(hb[4]);
-	uint32_t f4 = F_IPV4;
-	f4 |= ihl > 5u ? F_IPOPT : 0u;
-	f4 |= (frag & 0x3fffu) ? F_IPFRAG : 0u;
-	f4 |= dst == 0xffffffffu ? F_IP_BCAST : 0u;
-	f4 |= (dst >> 28) == 0xeu ? F_IP_MCAST : 0u;
-	const bool ok4 = is4 && !bad4;
-	f |= is4 ? (bad4 ? F_IPV4 : f4) : 0u;
-	// IPv6 (parse_ipv6, :174-246)
-	const uint32_t plen = bsw16(hb[1]);
-	const bool bad6 = ((hb[0] & 0xffu) >> 4) != 6u || 40u > len - l3 || plen + 40u > len - l3;
-	const uint32_t nh = (hb[1] >> 16) & 0xffu;
-	uint32_t f6 = F_IPV6;
-	f6 |= (hb[6] & 0xffu) == 0xffu ? F_IP_MCAST : 0u;
-	f6 |= nh == 44u ? (F_IPOPT | F_IPFRAG) : 0u;
-	const bool ok6 = is6 && !bad6;
-	f |= is6 ? (bad6 ? F_IPV6 : f6) : 0u;
-	err |= ((is4 && bad4) || (is6 && bad6)) ? E_IP : 0u;
-	const uint32_t ip_proto = ok4 ? ((hb[2] >> 8) & 0xffu) : (ok6 ? nh : ((is4 || is6) ? 0u : 255u));
-	const uint32_t l4 = ok4 ? l3 + ihl * 4u : (ok6 ? l3 + 40u : 0xFFFFu);
-	const bool non_first = ok4 && (frag & 0x1fffu) != 0u;
-	bool sl = ok6 && (nh == 0u || nh == 43u);   // extension chain: general parser
-
-	// L4 header bytes l4 .. l4+15 (dwords jl .. jl+4, byte shift 2)
-	const uint32_t jl = min((l4 - 2u) >> 2, (uint32_t)(WROWS - 5));
-	uint32_t m[5], lb[4];
-#pragma unroll
-	for (int i = 0; i < 5; ++i)
-		m[i] = k.w[(jl + i) * RS];
-#pragma unroll
-	for (int i = 0; i < 4; ++i)
-		lb[i] = __builtin_amdgcn_alignbyte(m[i + 1], m[i], 2u);
-	const bool tcp = ip_proto == 6u, udp = ip_proto == 17u, sctp = ip_proto == 132u;
-	sl = sl || ((tcp || udp || sctp) && !non_first && l4 + 18u > WIN);   // past the window
+	uint32_t ip_proto = (is4 || is6) ? 0u : 255u;   // bad IP header / no IP
+	uint32_t l4 = 0xFFFFu;
+	bool non_first = false, sl = false;
+	if (__ballot(is4) != 0ull) {
+		// IPv4 (parse_ipv4, odp_parse.c:112-167)
+		const uint32_t vi = hb[0] & 0xffu, ihl = vi & 0xfu;
+		const uint32_t tot = bsw16(hb[0] >> 16);
+		const bool bad4 = ihl < 5u || (vi >> 4) != 4u || 20u > len - l3 || tot > len - l3;
+		const uint32_t frag = bsw16(hb[1] >> 16);
+		const uint32_t dst = __builtin_bswap32(hb[4]);
+		uint32_t f4 = F_IPV4;
+		f4 |= ihl > 5u ? F_IPOPT : 0u;
+		f4 |= (frag & 0x3fffu) ? F_IPFRAG : 0u;
+		f4 |= dst == 0xffffffffu ? F_IP_BCAST : 0u;
+		f4 |= (dst >> 28) == 0xeu ? F_IP_MCAST : 0u;
+		const bool ok4 = is4 && !bad4;
+		f |= is4 ? (bad4 ? F_IPV4 : f4) : 0u;
+		err |= (is4 && bad4) ? E_IP : 0u;
+		ip_proto = ok4 ? ((hb[2] >> 8) & 0xffu) : ip_proto;
+		l4 = ok4 ? l3 + ihl * 4u : l4;
+		non_first = ok4 && (frag & 0x1fffu) != 0u;
+	}
+	if (__ballot(is6) != 0ull) {
+		// IPv6 (parse_ipv6, :174-246)
+		const uint32_t plen = bsw16(hb[1]);
+		const bool bad6 = ((hb[0] & 0xffu) >> 4) != 6u || 40u > len - l3 || plen + 40u > len - l3;
+		const uint32_t nh = (hb[1] >> 16) & 0xffu;
+		uint32_t f6 = F_IPV6;
+		f6 |= (hb[6] & 0xffu) == 0xffu ? F_IP_MCAST : 0u;
+		f6 |= nh == 44u ? (F_IPOPT | F_IPFRAG) : 0u;
+		const bool ok6 = is6 && !bad6;
+		f |= is6 ? (bad6 ? F_IPV6 : f6) : 0u;
+		err |= (is6 && bad6) ? E_IP : 0u;
+		ip_proto = ok6 ? nh : ip_proto;
+		l4 = ok6 ? l3 + 40u : l4;
+		sl = ok6 && (nh == 0u || nh == 43u);   // extension chain: general parser
+	}
 
 	// L4 (_odp_packet_parse_common_l3_l4, :395-460)
-	const bool icmp = ip_proto == 1u || ip_proto == 58u;
-	const bool ah = ip_proto == 51u, esp = ip_proto == 50u;
-	const bool known = icmp || tcp || udp || sctp || ah || esp || ip_proto == 4u || ip_proto == 59u;
-	f |= known ? F_L4 : 0u;
-	f |= icmp ? F_ICMP : 0u;
-	f |= tcp ? F_TCP : 0u;
-	f |= udp ? F_UDP : 0u;
-	f |= sctp ? F_SCTP : 0u;
-	f |= ah ? (F_IPSEC | F_AH) : 0u;
-	f |= esp ? (F_IPSEC | F_ESP) : 0u;
-	f |= ip_proto == 59u ? F_NO_NEXT : 0u;
-	const bool first = !non_first;
-	// TCP (parse_tcp, :299-316)
-	const bool tcp_drop = tcp && first && l4 + 20u > len;
-	err |= (tcp && first && !tcp_drop && ((lb[3] & 0xffu) >> 4) < 5u) ? E_TCP : 0u;
-	// UDP (parse_udp, :321-354)
-	const bool udp_drop = udp && first && l4 + 8u > len;
-	const uint32_t ulen = bsw16(lb[1]);
-	const bool udp_ok = udp && first && !udp_drop;
-	err |= (udp_ok && ulen < 8u) ? E_UDP : 0u;
-	f |= (udp_ok && ulen >= 8u && (lb[0] >> 16) == 0x9411u && ulen > 4u && lb[2] != 0u) ? F_IPSEC : 0u;
-	// SCTP (parse_sctp, :362-388)
-	const bool sctp_drop = sctp && first && l4 + 12u > len;
-	err |= (sctp && first && !sctp_drop && ((len - l4) & 0xffffu) < 12u) ? E_SCTP : 0u;
+	const uint32_t pt = l4tab[ip_proto];
+	f |= pt & 0x0fffffffu;
+	const uint32_t kc = pt >> 28;
+	const bool chk = kc != 0u && !non_first;   // a TCP / UDP / SCTP header to check
+	bool drop = false;
+	if (__ballot(chk) != 0ull) {
+		// L4 header bytes l4 .. l4+15 (dwords jl .. jl+4, byte shift 2)
+		const uint32_t jl = min((l4 - 2u) >> 2, (uint32_t)(WROWS - 5));
+		uint32_t m[5], lb[4];
+#pragma unroll
+		for (int i = 0; i < 5; ++i)
+			m[i] = k.w[(jl + i) * RS];
+#pragma unroll
+		for (int i = 0; i < 4; ++i)
+			lb[i] = __builtin_amdgcn_alignbyte(m[i + 1], m[i], 2u);
+		const bool tcp = chk && kc == L4K_TCP, udp = chk && kc == L4K_UDP;
+		const bool sctp = chk && kc == L4K_SCTP;
+		sl = sl || (chk && l4 + 18u > WIN);   // past the window
+		// TCP (parse_tcp, :299-316)
+		const bool tcp_drop = tcp && l4 + 20u > len;
+		err |= (tcp && !tcp_drop && ((lb[3] & 0xffu) >> 4) < 5u) ? E_TCP : 0u;
+		// UDP (parse_udp, :321-354)
+		const bool udp_drop = udp && l4 + 8u > len;
+		const uint32_t ulen = bsw16(lb[1]);
+		const bool udp_ok = udp && !udp_drop;
+		err |= (udp_ok && ulen < 8u) ? E_UDP : 0u;
+		f |= (udp_ok && ulen >= 8u && (lb[0] >> 16) == 0x9411u && ulen > 4u && lb[2] != 0u)
+			? F_IPSEC : 0u;
+		// SCTP (parse_sctp, :362-388)
+		const bool sctp_drop = sctp && l4 + 12u > len;
+		err |= (sctp && !sctp_drop && ((len - l4) & 0xffffu) < 12u) ? E_SCTP : 0u;
+		drop = tcp_drop || udp_drop || sctp_drop;
+	}
 
 	slow = sl;
 	r.l4 = l4;
 	r.flags = f;
 	r.err = err;
-	r.ret = (tcp_drop || udp_drop || sctp_drop) ? -1 : (err != 0u ? 1 : 0);
+	r.ret = drop ? -1 : (err != 0u ? 1 : 0);
 	return r;
 }
 
@@ -1112,6 +1153,7 @@ __global__ __launch_bounds__(NW * WAVE, MIN_WAVES_PER_EU) void mi_cls_kernel(KAr
 {
 	__shared__ uint32_t s_win[NW * RS * WROWS];
 	__shared__ uint32_t s_cnt[MAX_STATS_COS];
+	__shared__ uint32_t s_l4[256];
 
 	const uint32_t lane = threadIdx.x & (WAVE - 1);
 	const uint32_t wave = threadIdx.x >> 6;
@@ -1158,8 +1200,9 @@ __global__ __launch_bounds__(NW * WAVE, MIN_WAVES_PER_EU) void mi_cls_kernel(KAr
 		for (uint32_t i = threadIdx.x; i < MAX_STATS_COS; i += NW * WAVE)
 			s_cnt[i] = 0;
 	}
-	if (LT || stats_on)
-		__syncthreads();
+	for (uint32_t i = threadIdx.x; i < 256u; i += NW * WAVE)
+		s_l4[i] = c_l4tab.v[i];
+	__syncthreads();
 
 	// Software pipeline over this wave's tiles (64 packets each): while tile
 	// t is parsed and classified, tile t+1's header windows are in flight
@@ -1234,7 +1277,7 @@ __global__ __launch_bounds__(NW * WAVE, MIN_WAVES_PER_EU) void mi_cls_kernel(KAr
 
 		STAMP(1);   // next tile's loads issued
 		bool slow;
-		Parsed p = parse_fast(k, slow);
+		Parsed p = parse_fast(k, s_l4, slow);
 		if (__ballot(slow) != 0ull) {
 			if (slow)
 				p = parse_packet(k);
@@ -2058,8 +2101,8 @@ extern "C" int mi_cls_classify(mi_cls_ctx_t *c, const uint8_t *pkts, const uint3
 	const int wpb_env = c->wpb;
 	const size_t LDS_CU = 160u * 1024u;
 	const size_t hot_bytes = (size_t)c->hot_words * sizeof(uint32_t);
-	const size_t st4 = sizeof(uint32_t) * (4 * RS * WROWS + MAX_STATS_COS);
-	const size_t st16 = sizeof(uint32_t) * (16 * RS * WROWS + MAX_STATS_COS);
+	const size_t st4 = sizeof(uint32_t) * (4 * RS * WROWS + MAX_STATS_COS + 256);
+	const size_t st16 = sizeof(uint32_t) * (16 * RS * WROWS + MAX_STATS_COS + 256);
 	const bool fits16 = st16 + hot_bytes <= LDS_CU;
 	bool lt = (long)hot_bytes <= (long)hot_max;
 	// 4-wave blocks reach 4 blocks (16 waves) per CU only while four LDS
