@@ -43,11 +43,14 @@
 #ifndef WIN
 #define WIN 96             // staged header window, bytes (96 or 128)
 #endif
-#define WROWS (WIN / 4 + 1)     // LDS dword rows per wave window (+1 zero row)
+#define WROWS (WIN / 4 + 3)     // LDS dword rows per wave window (+3 zero rows)
 #define RS 66                   // LDS row stride of a window, dwords (see load_window)
 #define NPIECE (WIN / 16)       // 16-B pieces per window
 #ifndef MIN_WAVES_PER_EU
 #define MIN_WAVES_PER_EU 4
+#endif
+#ifndef LOAD_AUX
+#define LOAD_AUX 2          // cache policy of the packet-window loads: nt (read once)
 #endif
 #ifndef PREFETCH
 #define PREFETCH 1          // software-pipeline the next tile's loads
@@ -475,7 +478,7 @@ __device__ __forceinline__ Parsed parse_fast(const Pkt &k, const uint32_t *l4tab
 	bool drop = false;
 	if (__ballot(chk) != 0ull) {
 		// L4 header bytes l4 .. l4+15 (dwords jl .. jl+4, byte shift 2)
-		const uint32_t jl = min((l4 - 2u) >> 2, (uint32_t)(WROWS - 5));
+		const uint32_t jl = min((l4 - 2u) >> 2, (uint32_t)(WIN / 4 - 4));
 		uint32_t m[5], lb[4];
 #pragma unroll
 		for (int i = 0; i < 5; ++i)
@@ -511,24 +514,13 @@ __device__ __forceinline__ Parsed parse_fast(const Pkt &k, const uint32_t *l4tab
 }
 
 // --------------------------------------------------------- field registers
-// Gate bits (presence tests of the verify_pmr_<term> helpers)
-#define G_ETH   (1u << 0)
-#define G_VLAN0 (1u << 1)   // eth && vlan
-#define G_VLANX (1u << 2)   // vlan || qinq
-#define G_V4    (1u << 3)
-#define G_V6    (1u << 4)
-#define G_UDP   (1u << 5)
-#define G_TCP   (1u << 6)
-#define G_SPI   (1u << 7)   // ah || esp
-#define G_L3OK  (1u << 8)   // l2 && l3 valid
-
 // What the term verifiers compare is read on use from the packet window
 // (LDS; HBM past it) rather than cached in registers: the window stays valid
 // for the whole tile, and caching every kind the program might use would
-// hold ~20 VGPRs through the descent.  gates = presence bits of the fields.
+// hold ~20 VGPRs through the descent.
 struct Fields {
 	Pkt k;
-	uint32_t l3, l4, f, gates;
+	uint32_t l3, l4, f;
 };
 
 // Where the key words of a term kind sit (verify_pmr_<term>,
@@ -537,33 +529,38 @@ struct Fields {
 // (QinQ outer tag, IPv4 vs IPv6 next-header, AH vs ESP SPI); base is the
 // frame start, L3 or L4.  The term's mask words cut each word down to the
 // field (e.g. 0xffff for a 16-bit field), so every kind but LEN, PCP and
-// DSCP is "read words, AND mask".  gate: presence bits the packet needs.
+// DSCP is "read words, AND mask".  gate: the packet has the field iff its
+// flags share a bit with `gate` (~0: always).  The verifiers' presence tests
+// map onto single flag masks: eth && vlan is F_VLAN (both parsers set VLAN
+// only on frames that keep F_ETH), vlan || qinq, ipv4 || ipv6, ah || esp;
+// "l2 && l3 valid" (custom L3) is F_L2 plus the l3 != invalid test in
+// field_off.
 enum { FB_FRAME = 0, FB_L3 = 1, FB_L4 = 2 };
 struct FDesc {
 	uint32_t base, add, alt, altf, gate;
 };
 
-__device__ __forceinline__ FDesc fdesc(uint32_t kind, uint32_t toff)
+__host__ __device__ inline FDesc fdesc(uint32_t kind, uint32_t toff)
 {
 	FDesc d = { FB_FRAME, 0u, 0u, 0u, 0u };
 	switch (kind) {
-	case MI_K_ETH0: d = { FB_FRAME, 12u, 12u, 0u, G_ETH }; break;
-	case MI_K_ETHX: d = { FB_FRAME, 16u, 20u, F_QINQ, G_VLANX }; break;
-	case MI_K_VID0: d = { FB_FRAME, 14u, 14u, 0u, G_VLAN0 }; break;
-	case MI_K_VIDX: d = { FB_FRAME, 14u, 18u, F_QINQ, G_VLANX }; break;
-	case MI_K_DMAC: d = { FB_FRAME, 0u, 0u, 0u, G_ETH }; break;
-	case MI_K_PROTO: d = { FB_L3, 6u, 9u, F_IPV4, G_V4 | G_V6 }; break;
+	case MI_K_ETH0: d = { FB_FRAME, 12u, 12u, 0u, F_ETH }; break;
+	case MI_K_ETHX: d = { FB_FRAME, 16u, 20u, F_QINQ, F_VLAN | F_QINQ }; break;
+	case MI_K_VID0: d = { FB_FRAME, 14u, 14u, 0u, F_VLAN }; break;
+	case MI_K_VIDX: d = { FB_FRAME, 14u, 18u, F_QINQ, F_VLAN | F_QINQ }; break;
+	case MI_K_DMAC: d = { FB_FRAME, 0u, 0u, 0u, F_ETH }; break;
+	case MI_K_PROTO: d = { FB_L3, 6u, 9u, F_IPV4, F_IPV4 | F_IPV6 }; break;
 	case MI_K_UDP_DPORT:
-	case MI_K_UDP_SPORT: d = { FB_L4, 0u, 0u, 0u, G_UDP }; break;
+	case MI_K_UDP_SPORT: d = { FB_L4, 0u, 0u, 0u, F_UDP }; break;
 	case MI_K_TCP_DPORT:
-	case MI_K_TCP_SPORT: d = { FB_L4, 0u, 0u, 0u, G_TCP }; break;
-	case MI_K_SIP: d = { FB_L3, 12u, 12u, 0u, G_V4 }; break;
-	case MI_K_DIP: d = { FB_L3, 16u, 16u, 0u, G_V4 }; break;
-	case MI_K_SIP6: d = { FB_L3, 8u, 8u, 0u, G_V6 }; break;
-	case MI_K_DIP6: d = { FB_L3, 24u, 24u, 0u, G_V6 }; break;
-	case MI_K_SPI: d = { FB_L4, 0u, 4u, F_AH, G_SPI }; break;
+	case MI_K_TCP_SPORT: d = { FB_L4, 0u, 0u, 0u, F_TCP }; break;
+	case MI_K_SIP: d = { FB_L3, 12u, 12u, 0u, F_IPV4 }; break;
+	case MI_K_DIP: d = { FB_L3, 16u, 16u, 0u, F_IPV4 }; break;
+	case MI_K_SIP6: d = { FB_L3, 8u, 8u, 0u, F_IPV6 }; break;
+	case MI_K_DIP6: d = { FB_L3, 24u, 24u, 0u, F_IPV6 }; break;
+	case MI_K_SPI: d = { FB_L4, 0u, 4u, F_AH, F_AH | F_ESP }; break;
 	case MI_K_CUSTOM_FRAME: d = { FB_FRAME, toff, toff, 0u, ~0u }; break;
-	case MI_K_CUSTOM_L3: d = { FB_L3, toff, toff, 0u, G_L3OK }; break;
+	case MI_K_CUSTOM_L3: d = { FB_L3, toff, toff, 0u, F_L2 }; break;
 	default: break;
 	}
 	return d;
@@ -578,19 +575,18 @@ __device__ __forceinline__ bool kind_special(uint32_t kind)
 // LEN / PCP / DSCP values and presence (NEVER: absent, ALWAYS: present)
 __device__ __forceinline__ bool special_value(uint32_t kind, const Fields &x, uint32_t &v)
 {
-	const uint32_t g = x.gates;
 	if (kind == MI_K_LEN) {
 		v = x.k.len;
 		return true;
 	}
 	if (kind == MI_K_PCP0) {
 		v = (r16(x.k, 14) & 0xffu) >> 5;
-		return (g & G_VLAN0) != 0u;
+		return (x.f & F_VLAN) != 0u;
 	}
 	if (kind == MI_K_DSCP) {
 		v = (x.f & F_IPV4) ? (rb(x.k, x.l3 + 1) >> 2)
 				   : ((be32(x.k, x.l3) & 0x0fc00000u) >> 22);
-		return (g & (G_V4 | G_V6)) != 0u;
+		return (x.f & (F_IPV4 | F_IPV6)) != 0u;
 	}
 	v = 0;
 	return kind == MI_K_ALWAYS;
@@ -604,26 +600,12 @@ __device__ __forceinline__ uint32_t field_off(const FDesc &d, uint32_t kind, uin
 {
 	const uint32_t base = d.base == FB_L3 ? x.l3 : (d.base == FB_L4 ? x.l4 : 0u);
 	const uint32_t o = base + ((x.f & d.altf) ? d.alt : d.add);
-	present = d.gate == ~0u || (x.gates & d.gate) != 0u;
+	present = d.gate == ~0u || (x.f & d.gate) != 0u;
+	if (kind == MI_K_CUSTOM_L3)
+		present = present && x.l3 != 0xFFFFu;
 	if (kind == MI_K_CUSTOM_FRAME || kind == MI_K_CUSTOM_L3)
 		present = present && !(x.k.len <= o + size);
 	return o;
-}
-
-__device__ __forceinline__ uint32_t gates_of(const Parsed &p)
-{
-	const uint32_t f = p.flags;
-	uint32_t g = 0;
-	g |= (f & F_ETH) ? G_ETH : 0u;
-	g |= ((f & F_ETH) && (f & F_VLAN)) ? G_VLAN0 : 0u;
-	g |= (f & (F_VLAN | F_QINQ)) ? G_VLANX : 0u;
-	g |= (f & F_IPV4) ? G_V4 : 0u;
-	g |= (f & F_IPV6) ? G_V6 : 0u;
-	g |= (f & F_UDP) ? G_UDP : 0u;
-	g |= (f & F_TCP) ? G_TCP : 0u;
-	g |= (f & (F_AH | F_ESP)) ? G_SPI : 0u;
-	g |= ((f & F_L2) && p.l3 != 0xFFFFu) ? G_L3OK : 0u;
-	return g;
 }
 
 __device__ __forceinline__ Fields fields_of(const Pkt &k, const Parsed &p)
@@ -633,7 +615,6 @@ __device__ __forceinline__ Fields fields_of(const Pkt &k, const Parsed &p)
 	x.l3 = p.l3;
 	x.l4 = p.l4;
 	x.f = p.flags;
-	x.gates = gates_of(p);
 	return x;
 }
 
@@ -725,25 +706,39 @@ enum { DH_MAGIC = 0, DH_NCOS, DH_DEFAULT, DH_ERROR, DH_DEFAULT_VALID, DH_USED, D
 #define C_REC0 3u
 #define BV_MAX_CLS 8u
 #define BV_CLS_WORDS 16u
+#define BV_WIDE_WORDS 8u        // wide bitmap rows: up to 256 rules
+// class words 14-15: the field descriptor of the class's kind (fdesc()),
+// resolved at rule load so the device decodes it instead of switching on
+// kind: w14 = add | alt << 16; w15 = gate (flag mask, bits 0-23) | base << 24
+// | alt-flag code << 26 (1 QinQ, 2 IPv4, 3 AH) | BVF_* << 28
+#define BVC_AO 14u
+#define BVC_DESC 15u
+#define BVF_SPECIAL 1u          // LEN / PCP / DSCP: special_value()
+#define BVF_CUSTOM 2u           // custom frame / L3: length test
+#define BVF_L3 4u               // custom L3: l3 must be valid
 #define BV_EMPTY 0xFFFFFFFFu
 #define BV_NONE 0xFFFFFFFEu
 
 // Classification block of a CoS ("BV" block for historical reasons), used
 // when its rules fall into at most BV_MAX_CLS key classes (a key class is one
 // (term kind, mask[, offset, size]) combination).  build_bv() explains the
-// two modes; the layout (word indices into the hot region) is:
-//   b[0] mode (0 direct, 1 candidate, 2 bitmap), b[1] #classes, b[2] result words
-//   (dst | leaf<<8 | mark<<16 per rule; leaf = the destination CoS has no
-//   rules, so the descent ends there), b[3] first rule without a classified
-//   term (BV_NONE: none), b[4] rule records (bitmap: alive row), b[5]
-//   record words
+// modes; the layout (word indices into the hot region) is:
+//   b[0] mode (0 direct, 1 candidate, 2 bitmap, 3 wide bitmap), b[1] #classes,
+//   b[2] result words (dst | leaf<<8 | mark<<16 per rule; leaf = the
+//   destination CoS has no rules, so the descent ends there), b[3] first rule
+//   without a classified term (BV_NONE: none), b[4] rule records (bitmap:
+//   alive row; wide: block-relative index of the nw-word alive row), b[5]
+//   record words, b[6] wide: nw = words per row
 //   b[8 + 16 k ...] class k: kind, nkey, miss value (direct: first rule,
-//                   bitmap: row), offset, size, mask[4], #slots, table
-//                   offset, cuckoo multipliers m1, m2, list base
+//                   bitmap: row, wide: index of the miss row), offset, size,
+//                   mask[4], #slots, table offset, cuckoo multipliers m1, m2,
+//                   list base
 //   table slot (nkey + 1 words): key words, value (0: empty)
 //     direct: 1 + first live rule with this key or without a term of the
 //             class (BV_EMPTY: none)
 //     bitmap: the 32-bit row of rules with this key or without a term
+//     wide:   index of the nw-word row of rules with this key or without a
+//             term of the class (rows are deduplicated)
 //     candidate: key id | list length << 12 | list offset << 20; the list
 //             holds the rules filed under this key, in scan order
 //   rule record (candidate, 1 + ceil(#classes / 2) words): constrained-
@@ -809,23 +804,30 @@ template <typename D>
 __device__ __forceinline__ bool bv_key(const D &cr, const Pkt &k, const Parsed &p, const Fields &x,
 				       uint32_t key[4])
 {
-	const uint32_t kind = cr(0), nk = cr(1);
+	const uint32_t nk = cr(1), desc = cr(BVC_DESC), dfl = desc >> 28;
 	key[0] = key[1] = key[2] = key[3] = 0;
-	if (kind_special(kind)) {
+	if (dfl & BVF_SPECIAL) {
 		uint32_t v;
-		const bool pr = special_value(kind, x, v);
+		const bool pr = special_value(cr(0), x, v);
 		key[0] = v & cr(5);
 		return pr;
 	}
-	const FDesc d = fdesc(kind, cr(3));
-	bool present;
-	const uint32_t o = field_off(d, kind, cr(4), x, present);
+	// the class's field descriptor (fdesc() of its kind, resolved at load)
+	const uint32_t ao = cr(BVC_AO), fb = (desc >> 24) & 3u, ac = (desc >> 26) & 3u;
+	const uint32_t altf = ac == 1u ? F_QINQ : (ac == 2u ? F_IPV4 : (ac == 3u ? F_AH : 0u));
+	const uint32_t base = fb == FB_L3 ? x.l3 : (fb == FB_L4 ? x.l4 : 0u);
+	const uint32_t o = base + ((x.f & altf) ? (ao >> 16) : (ao & 0xffffu));
+	bool present = (x.f & desc & 0xffffffu) != 0u;
+	if (dfl & BVF_CUSTOM)   // verify_pmr_custom_*: the frame extends past the field
+		present = present && ((dfl & BVF_L3) == 0u || x.l3 != 0xFFFFu) &&
+			  !(x.k.len <= o + cr(4));
 	key[0] = r32(k, o) & cr(5);
-	if (nk > 1)
+	if (nk > 1u) {
 		key[1] = r32(k, o + 4u) & cr(6);
-	if (nk > 2) {
-		key[2] = r32(k, o + 8u) & cr(7);
-		key[3] = r32(k, o + 12u) & cr(8);
+		if (nk > 2u) {
+			key[2] = r32(k, o + 8u) & cr(7);
+			key[3] = r32(k, o + 12u) & cr(8);
+		}
 	}
 	return present;
 }
@@ -837,16 +839,26 @@ __device__ __forceinline__ bool bv_key(const D &cr, const Pkt &k, const Parsed &
 template <typename D, typename T>
 __device__ __forceinline__ uint32_t bv_lookup(const D &cr, T H, const uint32_t key[4], bool act)
 {
-	const uint32_t nk = cr(1), ns = cr(9), tbl = cr(10);
+	const uint32_t nk = cr(1), ns = cr(9), tbl = cr(10), m1 = cr(11), m2 = cr(12);
+	uint32_t val = 0;
+	if (nk == 1u) {
+		// one-word keys (the common case): bv_fold with zero upper words,
+		// two-word slots
+		uint32_t f = key[0] * 0x9E3779B1u;
+		f ^= f >> 15;
+		const uint32_t a1 = tbl + 2u * __umulhi(f * m1, ns);
+		const uint32_t a2 = tbl + 2u * __umulhi(f * m2, ns);
+		const uint32_t k1 = H[a1], v1 = H[a1 + 1u], k2 = H[a2], v2 = H[a2 + 1u];
+		val = (k2 == key[0]) ? v2 : 0u;
+		val = (k1 == key[0] && v1 != 0u) ? v1 : val;
+		return act ? val : 0u;
+	}
 	const uint32_t f = bv_fold(key);
 	const uint32_t sw = nk + 1u;
-	uint32_t val = 0;
 #pragma unroll
 	for (uint32_t s = 0; s < 2; ++s) {
-		const uint32_t a = tbl + __umulhi(f * cr(11u + s), ns) * sw;
-		bool e = H[a] == key[0];
-		if (nk > 1)
-			e = e && H[a + 1] == key[1];
+		const uint32_t a = tbl + __umulhi(f * (s ? m2 : m1), ns) * sw;
+		bool e = H[a] == key[0] && H[a + 1] == key[1];
 		if (nk > 2)
 			e = e && H[a + 2] == key[2] && H[a + 3] == key[3];
 		const uint32_t v = H[a + nk];
@@ -889,6 +901,32 @@ __device__ __forceinline__ void bv_eval(const D &blk, T H, bool act, const Pkt &
 			}
 		}
 		first = acc != 0u ? (uint32_t)__builtin_ctz(acc) : BV_NONE;
+	} else if (mode == 3u) {
+		// wide bitmap (33..256 rules): AND of the classes' rows (in the hot
+		// region, BV_WIDE_WORDS words each, zero past the rule count; a miss
+		// takes the class's miss row) and the alive row; the lowest set bit
+		// is the first holding rule
+		const uint32_t ar = blk(4);
+		uint32_t acc[BV_WIDE_WORDS];
+#pragma unroll
+		for (uint32_t i = 0; i < BV_WIDE_WORDS; ++i)
+			acc[i] = blk(ar + i);
+#pragma unroll
+		for (uint32_t kc = 0; kc < BV_MAX_CLS; ++kc) {
+			if (kc < ncls) {
+				const D cr = blk.at(8u + BV_CLS_WORDS * kc);
+				uint32_t key[4];
+				const bool present = bv_key(cr, k, p, x, key);
+				const uint32_t val = bv_lookup(cr, H, key, act && present);
+				const uint32_t ro = val != 0u ? val : cr(2);
+#pragma unroll
+				for (uint32_t i = 0; i < BV_WIDE_WORDS; ++i)
+					acc[i] &= H[ro + i];
+			}
+		}
+#pragma unroll
+		for (int i = (int)BV_WIDE_WORDS - 1; i >= 0; --i)
+			first = acc[i] != 0u ? 32u * (uint32_t)i + (uint32_t)__builtin_ctz(acc[i]) : first;
 	} else {
 		// candidate: key id per class, then the candidates' records
 		const uint32_t rec0 = blk(4), rw = blk(5);
@@ -1048,7 +1086,7 @@ __device__ __forceinline__ bool load_window(__amdgpu_buffer_rsrc_t rs, uint32_t 
 		const uint32_t o = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)off);
 		const uint32_t L = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)len);
 		const uint32_t vo = 16u * q < L ? o + 16u * q : OOB_OFF;
-		d[r] = __builtin_amdgcn_raw_buffer_load_b128(rs, vo, 0, 0);
+		d[r] = __builtin_amdgcn_raw_buffer_load_b128(rs, vo, 0, LOAD_AUX);
 	}
 	const bool hi = __ballot(len > 64u) != 0ull;
 	if (hi) {
@@ -1060,7 +1098,7 @@ __device__ __forceinline__ bool load_window(__amdgpu_buffer_rsrc_t rs, uint32_t 
 			const uint32_t L = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)len);
 			const uint32_t c = 16u * (4u + qb);
 			const uint32_t vo = c < L ? o + c : OOB_OFF;
-			d[4 + r] = __builtin_amdgcn_raw_buffer_load_b128(rs, vo, 0, 0);
+			d[4 + r] = __builtin_amdgcn_raw_buffer_load_b128(rs, vo, 0, LOAD_AUX);
 		}
 	}
 	return hi;
@@ -1101,27 +1139,26 @@ __device__ __forceinline__ void store_window(uint32_t *W, uint32_t lane, const u
 }
 
 // Zero the bytes of the last loaded piece that lie past the frame
-// (frame_len .. end of its 16-B piece): the partial dword byte by byte, then
-// up to three whole dwords.  Writes that are not needed go to the lane's pad
-// dword, which is zero anyway, so every lane issues the same 6 stores.
+// (frame_len .. end of its 16-B piece; loaded pieces wholly past the frame
+// read as zero already): bytes b..3 of the partial dword with one byte store
+// (b odd) and one 16-bit store (b <= 2) -- stores that are not needed go to
+// the lane's pad dword, which is zero anyway -- then the next three whole
+// dwords without a test: rows past the piece are zero (pieces past the
+// frame, or the zero rows WIN/4 .. WIN/4+2 where a frame of >= WIN bytes
+// starts).
 __device__ __forceinline__ void zero_tail(uint32_t *W, uint32_t lane, uint32_t len)
 {
 	const uint32_t pad = (WIN / 4) * RS + lane;
-	const uint32_t e = min((len + 15u) & ~15u, (uint32_t)WIN);   // end of loaded bytes
 	const uint32_t dw = len >> 2, b = len & 3u;
+	const bool part = b != 0u && len < WIN;
 	uint8_t *W8 = (uint8_t *)W;
-#pragma unroll
-	for (uint32_t j = 1; j < 4; ++j) {
-		const bool z = b != 0u && j >= b && len < WIN;
-		const uint32_t at = z ? (dw * RS + lane) * 4u + j : pad * 4u + j;
-		W8[at] = 0;
-	}
-	const uint32_t pd = (len + 3u) >> 2;
-#pragma unroll
-	for (uint32_t i = 0; i < 3; ++i) {
-		const bool z = 4u * (pd + i) < e;
-		W[z ? (pd + i) * RS + lane : pad] = 0u;
-	}
+	const uint32_t pb = (dw * RS + lane) * 4u;
+	W8[(part && (b & 1u)) ? pb + b : pad * 4u + 1u] = 0;
+	*(uint16_t *)(W8 + ((part && b <= 2u) ? pb + 2u : pad * 4u + 2u)) = 0;
+	uint32_t *z = W + min((len + 3u) >> 2, (uint32_t)(WIN / 4)) * RS + lane;
+	z[0] = 0u;
+	z[RS] = 0u;
+	z[2 * RS] = 0u;
 }
 
 // Make this wave's LDS writes visible to its own later LDS reads by other
@@ -1167,6 +1204,10 @@ __global__ __launch_bounds__(NW * WAVE, MIN_WAVES_PER_EU) void mi_cls_kernel(KAr
 	const uint32_t hot_off = dev[DH_HOT_OFF];
 	const cword_t hc = dev + hot_off;                 // hot region, scalar reads
 	const cword_t prog = dev + dev[DH_PROG_OFF];
+	// the default CoS's words (the first descent round always evaluates it)
+	const cword_t dce = hc + COS_WORDS * (uint32_t)max(def_cos, 0);
+	const uint32_t d_nr = def_cos >= 0 ? dce[C_NR] : 0u;
+	const uint32_t d_bv = dce[C_BV], d_rec0 = dce[C_REC0];
 	const bool stats_on = a.stats != nullptr;
 	typedef typename std::conditional<LT, lword_t, gword_t>::type hot_t;
 	hot_t H;
@@ -1215,7 +1256,8 @@ __global__ __launch_bounds__(NW * WAVE, MIN_WAVES_PER_EU) void mi_cls_kernel(KAr
 		(void *)a.pkts, (short)0, (int)OOB_OFF, 0x00020000);
 	u32x4 d[NPIECE];
 	bool d_hi, hi_rows = true;
-	W[(WIN / 4) * RS + lane] = 0u;   // pad row: always zero
+	for (uint32_t r = WIN / 4; r < WROWS; ++r)
+		W[r * RS + lane] = 0u;   // pad / zero rows: always zero
 	uint4 prev_rec = make_uint4(0, 0, 0, 0);
 	uint32_t prev_pi = 0;
 	bool prev_valid = false;
@@ -1288,7 +1330,7 @@ __global__ __launch_bounds__(NW * WAVE, MIN_WAVES_PER_EU) void mi_cls_kernel(KAr
 			uint4 rec;
 			rec.x = p.flags;
 			rec.y = p.err;
-			rec.z = x.gates;
+			rec.z = x.f ^ x.l4;
 			rec.w = (p.l3 & 0xffffu) | ((p.l4 & 0xffffu) << 16);
 			*(uint4 *)(a.out + pi) = rec;
 		}
@@ -1311,6 +1353,35 @@ __global__ __launch_bounds__(NW * WAVE, MIN_WAVES_PER_EU) void mi_cls_kernel(KAr
 		// the CoS's words in SGPRs); in tree programs (DIV) lanes on other
 		// bit-vector CoS evaluate their own blocks in the same round.
 		uint32_t hops = 0, mark = 0, matched = 0, loop = 0;
+		// one hop of the lanes in `proc` whose evaluation gave hit / nxt / ..
+		auto advance = [&](uint32_t proc, uint32_t hit, uint32_t nxt, uint32_t nmark,
+				   uint32_t nleaf) {
+			const uint32_t take = proc & hit;
+			cur = take ? (int32_t)nxt : cur;
+			mark = take ? nmark : mark;
+			matched |= take;
+			hops += take;
+			const uint32_t lp = (take != 0u && hops > max_hops) ? 1u : 0u;
+			loop |= lp;
+			// still pending: a rule matched, under the hop limit, and the
+			// destination CoS has rules
+			pend = proc ? ((take != 0u && lp == 0u && nleaf == 0u) ? 1u : 0u) : pend;
+			if (stats_on) {
+				if (take != 0u && stats_bit(a, nxt))
+					atomicAdd(&s_cnt[nxt], 1u);
+			}
+		};
+		// round 1: every pending lane sits on the default CoS, whose words
+		// are loop-invariant (d_nr / d_bv / d_rec0, loaded once per wave)
+		if (__ballot(pend != 0u) != 0ull) {
+			uint32_t hit = 0, nleaf = 0, nxt = 0, nmark = 0;
+			const bool g = pend != 0u;
+			if (d_bv != 0u && d_nr != 0u)
+				bv_eval(DescU{ hc + d_bv }, H, g, k, p, x, hit, nxt, nmark, nleaf);
+			else
+				linear_scan(prog, d_rec0, d_nr, g, k, p, x, hit, nxt, nmark);
+			advance(g ? 1u : 0u, hit, nxt, nmark, nleaf);
+		}
 		for (;;) {
 			const unsigned long long pm = __ballot(pend != 0u);
 			if (pm == 0ull)
@@ -1345,24 +1416,21 @@ __global__ __launch_bounds__(NW * WAVE, MIN_WAVES_PER_EU) void mi_cls_kernel(KAr
 				else
 					linear_scan(prog, ce[C_REC0], nr, g, k, p, x, hit, nxt, nmark);
 			}
-			const uint32_t proc = handled | grp;
-			const uint32_t take = proc & hit;
-			cur = take ? (int32_t)nxt : cur;
-			mark = take ? nmark : mark;
-			matched |= take;
-			hops += take;
-			const uint32_t lp = (take != 0u && hops > max_hops) ? 1u : 0u;
-			loop |= lp;
-			// still pending: a rule matched, under the hop limit, and the
-			// destination CoS has rules
-			pend = proc ? ((take != 0u && lp == 0u && nleaf == 0u) ? 1u : 0u) : pend;
-			if (stats_on) {
-				if (take != 0u && stats_bit(a, nxt))
-					atomicAdd(&s_cnt[nxt], 1u);
-			}
+			advance(handled | grp, hit, nxt, nmark, nleaf);
 		}
 
 		STAMP(3);   // descent done
+#ifdef DIAG_DESCENTONLY
+		if (valid) {
+			uint4 rec;
+			rec.x = (uint32_t)cur;
+			rec.y = mark;
+			rec.z = hops | (matched << 8) | (loop << 9);
+			rec.w = p.flags;
+			*(uint4 *)(a.out + pi) = rec;
+		}
+		continue;
+#endif
 		// ---- final CoS -> outcome / queue (_odp_cls_classify_packet, :1742-1771)
 		const bool mk = matched != 0u && loop == 0u;
 		const uint32_t flags = mk ? ((p.flags & ~F_CLS_MARK) | (mark ? F_CLS_MARK : 0u)) : p.flags;
@@ -1774,7 +1842,10 @@ static bool build_bv(const mi_cos_t *cs, const mi_rule_t *rs, const mi_term_t *t
 			if ((tmask[r] >> c) & 1u)
 				freq[c][want[r][c]]++;
 	}
-	const uint32_t mode = ncls == 1 ? 0u : (nrules <= 32 ? 2u : 1u);
+	// MI_CLS_NO_WIDE: candidate lists instead of wide rows (A/B, tests)
+	const bool wide_ok = getenv("MI_CLS_NO_WIDE") == nullptr;
+	const uint32_t mode = ncls == 1 ? 0u
+		: (nrules <= 32 ? 2u : ((wide_ok && nrules <= 32 * BV_WIDE_WORDS) ? 3u : 1u));
 	std::vector<std::map<Key4, uint32_t>> kid(ncls);   // value -> key id (1..)
 	for (uint32_t c = 0; c < ncls; ++c) {
 		uint32_t id = 1;
@@ -1800,11 +1871,40 @@ static bool build_bv(const mi_cos_t *cs, const mi_rule_t *rs, const mi_term_t *t
 		blk.push_back((rs[r].dst_cos & 0xffu) | (cs[rs[r].dst_cos].num_rules == 0 ? 0x100u : 0u) |
 			      ((uint32_t)rs[r].mark << 16));
 	std::vector<std::vector<std::vector<uint32_t>>> lists(ncls);   // [class][key id] -> rules
+	// wide rows: nw words each, deduplicated, appended to the block; a row's
+	// value is its hot-region word index (non-zero: the CoS table comes first)
+	const uint32_t nw = (nrules + 31u) / 32u;
+	std::map<std::vector<uint32_t>, uint32_t> row_at;
+	auto put_row = [&](const std::vector<uint32_t> &row) -> uint32_t {
+		auto it = row_at.find(row);
+		if (it != row_at.end())
+			return it->second;
+		const uint32_t at = base + (uint32_t)blk.size();
+		blk.insert(blk.end(), row.begin(), row.end());
+		row_at[row] = at;
+		return at;
+	};
+	auto wide_row = [&](uint32_t c, const Key4 *v) {
+		std::vector<uint32_t> w(BV_WIDE_WORDS, 0u);   // zero past the rule count
+		for (uint32_t r = 0; r < nrules; ++r)
+			if (holds_class(r, c, v))
+				w[r / 32u] |= 1u << (r % 32u);
+		return w;
+	};
 	if (mode == 2u) {
 		uint32_t aw = 0;
 		for (uint32_t r = 0; r < nrules; ++r)
 			aw |= (uint32_t)alive[r] << r;
 		blk[4] = aw;
+	} else if (mode == 3u) {
+		blk[6] = nw;
+		blk[4] = (uint32_t)blk.size();   // the alive row, block-relative
+		for (uint32_t i = 0; i < BV_WIDE_WORDS; ++i) {
+			uint32_t aw = 0;
+			for (uint32_t j = 0; j < 32u && 32u * i + j < nrules; ++j)
+				aw |= (uint32_t)alive[32u * i + j] << j;
+			blk.push_back(aw);
+		}
 	} else if (mode == 1u) {
 		const uint32_t RW = 1u + (ncls + 1u) / 2u;
 		blk[4] = base + (uint32_t)blk.size();
@@ -1860,7 +1960,10 @@ static bool build_bv(const mi_cos_t *cs, const mi_rule_t *rs, const mi_term_t *t
 		const uint32_t SW = ck.nkey + 1u;   // slot: key words, value
 		blk[cbase + 0] = ck.kind;
 		blk[cbase + 1] = ck.nkey;
-		blk[cbase + 2] = mode == 0u ? first_live(c, nullptr) : (mode == 2u ? row_of(c, nullptr) : 0u);
+		// (put_row grows blk: compute before indexing it)
+		const uint32_t miss = mode == 0u ? first_live(c, nullptr)
+			: (mode == 2u ? row_of(c, nullptr) : (mode == 3u ? put_row(wide_row(c, nullptr)) : 0u));
+		blk[cbase + 2] = miss;
 		blk[cbase + 3] = ck.offset;
 		blk[cbase + 4] = ck.size;
 		for (int i = 0; i < 4; ++i)
@@ -1868,6 +1971,23 @@ static bool build_bv(const mi_cos_t *cs, const mi_rule_t *rs, const mi_term_t *t
 		blk[cbase + 9] = nb;
 		blk[cbase + 11] = m1;
 		blk[cbase + 12] = m2;
+		{
+			const bool special = ck.kind == MI_K_LEN || ck.kind == MI_K_PCP0 ||
+					     ck.kind == MI_K_DSCP;
+			const FDesc d = fdesc(ck.kind, ck.offset);
+			if (d.add > 0xffffu || d.alt > 0xffffu)
+				return false;   // custom offset past 64 KiB: linear scan
+			// "always present" (custom frame) is F_L2, which every parsed
+			// frame has
+			const uint32_t gate = d.gate == ~0u ? F_L2 : d.gate;
+			const uint32_t ac = d.altf == F_QINQ ? 1u
+				: (d.altf == F_IPV4 ? 2u : (d.altf == F_AH ? 3u : 0u));
+			const uint32_t fl = (special ? BVF_SPECIAL : 0u) |
+				((ck.kind == MI_K_CUSTOM_FRAME || ck.kind == MI_K_CUSTOM_L3) ? BVF_CUSTOM : 0u) |
+				(ck.kind == MI_K_CUSTOM_L3 ? BVF_L3 : 0u);
+			blk[cbase + BVC_AO] = d.add | (d.alt << 16);
+			blk[cbase + BVC_DESC] = (gate & 0xffffffu) | (d.base << 24) | (ac << 26) | (fl << 28);
+		}
 		const uint32_t tbl_off = (uint32_t)blk.size();
 		blk[cbase + 10] = base + tbl_off;
 		// empty slots keep key words 0 and value 0: a miss (every stored
@@ -1894,6 +2014,8 @@ static bool build_bv(const mi_cos_t *cs, const mi_rule_t *rs, const mi_term_t *t
 				val = f == BV_NONE ? BV_EMPTY : f + 1u;
 			} else if (mode == 2u) {
 				val = row_of(c, &keys[i]);   // non-zero: the key's own rules
+			} else if (mode == 3u) {
+				val = put_row(wide_row(c, &keys[i]));   // word index, non-zero
 			} else {
 				const uint32_t id = kid[c][keys[i]];
 				uint32_t off = 0;

@@ -23,6 +23,7 @@ ENGINE_ENV = {
     "div": {"MI_CLS_DIV": "1"},        # per-lane bit-vector rounds even for flat programs
     "wpb4": {"MI_CLS_WPB": "4"},       # 4-wave blocks (own hot-region copy or HBM)
     "wpb16": {"MI_CLS_WPB": "16"},     # one 16-wave block per CU sharing the LDS copy
+    "nowide": {"MI_CLS_NO_WIDE": "1"},  # candidate lists instead of wide bitmap rows
 }
 
 
@@ -31,7 +32,7 @@ def both(prog, batch, limits=(255, 8192, 4096), what="", engine="auto"):
     linear scan otherwise, per-lane rounds for CoS trees; the other engines
     force one of the kernel's paths (ENGINE_ENV)."""
     import os
-    keys = ("MI_CLS_NO_BV", "MI_CLS_DIV", "MI_CLS_WPB")
+    keys = ("MI_CLS_NO_BV", "MI_CLS_DIV", "MI_CLS_WPB", "MI_CLS_NO_WIDE")
     old = {k: os.environ.pop(k, None) for k in keys}
     os.environ.update(ENGINE_ENV[engine])
     try:
@@ -94,7 +95,7 @@ def test_zoo_no_default(built, gpu):
     assert s["discard"] > 0 and s["cos_drop"] > 0
 
 
-@pytest.mark.parametrize("engine", ["auto", "linear", "nodiv", "div", "wpb16"])
+@pytest.mark.parametrize("engine", ["auto", "linear", "nodiv", "div", "wpb16", "nowide"])
 @pytest.mark.parametrize("seed", range(12))
 def test_random_programs_fuzz(built, gpu, seed, engine):
     rng = np.random.default_rng(1000 + seed)
@@ -107,13 +108,22 @@ def test_random_programs_fuzz(built, gpu, seed, engine):
     both(prog, b, what=f"fuzz seed {seed}", engine=engine)
 
 
-@pytest.mark.parametrize("engine", ["auto", "linear", "nodiv", "wpb4", "wpb16"])
+@pytest.mark.parametrize("engine", ["auto", "linear", "nodiv", "wpb4", "wpb16", "nowide"])
 @pytest.mark.parametrize("cfg,n", [(1, 10_000), (2, 100_000), (3, 50_000), (4, 50_000),
                                    (5, 20_000)])
 def test_configs_small(built, gpu, cfg, n, engine):
     b, prog = R.CONFIGS[cfg](n)
     got = both(prog, b, what=f"config {cfg}", engine=engine)
     assert summary(got)["enq"] > 0
+
+
+@pytest.mark.parametrize("engine", ["auto", "nowide", "div"])
+@pytest.mark.parametrize("num_rules", [33, 64, 100, 200, 255, 256, 257])
+def test_wide_rule_counts(built, gpu, num_rules, engine):
+    """Rule counts around the wide-bitmap engine's word boundaries (33..256
+    rules on one CoS) and just past it (257: candidate lists)."""
+    b, prog = R.config3(20_000, num_rules=num_rules, size=60)
+    both(prog, b, what=f"{num_rules} rules", engine=engine)
 
 
 def test_config2_tree_equals_flat(built, gpu):

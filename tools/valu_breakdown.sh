@@ -7,10 +7,10 @@ ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/valu
 mkdir -p $OUT
 i=0
-for v in "DIAG_STAGEONLY $*" "DIAG_PARSEONLY $*" "VB_FULL $*"; do
+for v in "DIAG_STAGEONLY $*" "DIAG_PARSEONLY $*" "DIAG_DESCENTONLY $*" "VB_FULL $*"; do
   d=/tmp/vb_$i
   timeout -k 10 300 python -m odp_amd._build $d $v > /dev/null || exit 1
-  for c in 20 2; do
+  for c in ${VB_CFGS:-20 2}; do
     ( cd /tmp && export TMPDIR=/tmp && ODP_AMD_LIB_DIR=$d timeout -k 10 200 rocprofv3 \
       --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_WAVES \
       --output-format csv -d $OUT/b${i}_c$c -o p -- python3 $ROOT/bench.py --config $c --steps 5 \
