@@ -195,6 +195,17 @@ int mi_cls_classify_host(mi_cls_ctx_t *ctx, const uint8_t *pkts_host, size_t byt
 			 const uint32_t *off_host, const uint16_t *len_host, uint32_t n,
 			 mi_cls_result_t *out_host);
 
+/* pktin parse options for the following classify calls on this context:
+ * odp_pktin_config_opt_t.all_bits (include/odp_rt.h; reference
+ * include/odp/api/spec/packet_io.h odp_pktin_config_opt_t).  Bits 2-5
+ * validate the IPv4 header / UDP / TCP / SCTP checksums (odp_parse.c:134-141,
+ * 298-313, odp_packet.c:2065-2138: l3/l4_chksum_done in in_flags bits 30/31,
+ * l3/l4_chksum_err in err bits 2/6), bits 6-10 drop packets with IPv4 /
+ * IPv6 / UDP / TCP / SCTP errors (MI_CLS_OUT_PARSE_DROP).  0 (the default)
+ * is the plain parse.  Replaces the `opt` argument of
+ * _odp_packet_parse_common (include/odp_parse_internal.h:80-112). */
+int mi_cls_pktin_opt_set(mi_cls_ctx_t *ctx, uint64_t opt);
+
 /* Pinned (page-locked) host memory for staging; NULL on failure. */
 void *mi_cls_host_alloc(size_t bytes);
 void mi_cls_host_free(void *p);

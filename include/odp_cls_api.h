@@ -295,6 +295,12 @@ int odp_amd_cls_classify_host(odp_pktio_t pktio, const uint8_t *pkts, size_t byt
  * warm-up launch (odp_pktio_start). */
 int odp_amd_cls_prepare(odp_pktio_t pktio, int parse_only);
 
+/* pktin parse options of the pktio (odp_pktin_config_opt_t.all_bits, from
+ * odp_pktio_config(): checksum validation and drop-on-error bits), applied
+ * by every later classify call: the `opt` that loop.c:271/310 hands to
+ * _odp_packet_parse_common (include/odp_parse_internal.h:80-112). */
+int odp_amd_cls_pktin_opt_set(odp_pktio_t pktio, uint64_t opt);
+
 /* Enqueue-stage counters of a (CoS, queue slot) (odp_cls_queue_stats). */
 void odp_amd_cls_queue_stats_add(uint32_t cos_index, uint32_t slot, uint64_t packets,
 				 uint64_t discards);

@@ -467,6 +467,17 @@ int odp_packet_has_error(odp_packet_t pkt);
 int odp_packet_has_l2_error(odp_packet_t pkt);
 int odp_packet_has_l3_error(odp_packet_t pkt);
 int odp_packet_has_l4_error(odp_packet_t pkt);
+
+/* Checksum check status (include/odp/api/spec/packet_types.h, values from
+ * the receive parse with pktin checksum options, packet_inlines.h:389-420) */
+typedef enum {
+	ODP_PACKET_CHKSUM_UNKNOWN = 0,
+	ODP_PACKET_CHKSUM_BAD,
+	ODP_PACKET_CHKSUM_OK
+} odp_packet_chksum_status_t;
+
+odp_packet_chksum_status_t odp_packet_l3_chksum_status(odp_packet_t pkt);
+odp_packet_chksum_status_t odp_packet_l4_chksum_status(odp_packet_t pkt);
 int odp_packet_has_l2(odp_packet_t pkt);
 int odp_packet_has_l3(odp_packet_t pkt);
 int odp_packet_has_l4(odp_packet_t pkt);

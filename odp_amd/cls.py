@@ -135,6 +135,7 @@ def _load():
         "odp_amd_cls_classify": (i32, [vp, vp, vp, vp, u32, vp, vp]),
         "odp_amd_cls_queue_of": (vp, [u32, u32]),
         "odp_amd_cls_generation": (C.c_uint64, []),
+        "odp_amd_cls_pktin_opt_set": (i32, [vp, C.c_uint64]),
         "mi_cls_device_count": (i32, []),
         "mi_cls_ctx_create": (i32, [i32, C.POINTER(vp)]),
         "mi_cls_ctx_destroy": (i32, [vp]),
@@ -248,6 +249,13 @@ class Classifier:
             else:
                 raise ValueError(op)
         return self.cos, self.pmr
+
+    def set_pktin_opt(self, opt: int):
+        """pktin parse options of this receive endpoint
+        (odp_pktin_config_opt_t.all_bits: bits 2-5 IPv4/UDP/TCP/SCTP
+        checksum validation, bits 6-10 drop on IPv4/IPv6/UDP/TCP/SCTP
+        errors)."""
+        assert self.L.odp_amd_cls_pktin_opt_set(self.pktio, int(opt)) == 0
 
     def compile(self) -> bytes:
         n = self.L.odp_amd_cls_compile(self.pktio, None, 0)

@@ -90,12 +90,29 @@
 #define E_TCP  8u
 #define E_UDP  16u
 #define E_SCTP 32u
+#define E_L3CK 4u           // l3_chksum_err
+#define E_L4CK 64u          // l4_chksum_err
+#define F_L3CK_DONE (1u << 30)   // input_flags.l3_chksum_done
+#define F_L4CK_DONE (1u << 31)   // input_flags.l4_chksum_done
+// pktin options: odp_pktin_config_opt_t.all_bits (include/odp_rt.h)
+#define OPT_IPV4_CK (1u << 2)
+#define OPT_UDP_CK (1u << 3)
+#define OPT_TCP_CK (1u << 4)
+#define OPT_SCTP_CK (1u << 5)
+#define OPT_DROP_V4 (1u << 6)
+#define OPT_DROP_V6 (1u << 7)
+#define OPT_DROP_UDP (1u << 8)
+#define OPT_DROP_TCP (1u << 9)
+#define OPT_DROP_SCTP (1u << 10)
+#define OPT_L4_CK (OPT_UDP_CK | OPT_TCP_CK | OPT_SCTP_CK)
 
 // ------------------------------------------------------- packet byte access
 // The LDS window of a wave is dword-major, lane-minor: dword i of lane l's
 // packet lives at W[i * RS + l] (RS = 66).  Any per-lane byte offset then
 // reads conflict-free (lane l of row i hits bank 2i + l mod 32), whatever the
 // packets' header layouts.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
 struct Pkt {
 	const uint32_t *w;      // &W[lane]
 	const uint8_t *g;       // packet start in HBM
@@ -141,16 +158,30 @@ struct Parsed {
 	uint32_t err;
 	uint32_t l3, l4;
 	int ret;                // 0 ok, 1 error flags, -1 drop
+	uint32_t udp_zero;      // input_flags.udp_chksum_zero (bit 32: not stored)
 };
 
-// _odp_parse_eth + _odp_packet_parse_common_l3_l4 (layer ALL, checksum opts off),
-// odp_parse.c:23-105, 112-354, 362-488; contiguous packet so seg_end == frame_len.
-__device__ __forceinline__ Parsed parse_packet(const Pkt &k)
+// one's-complement fold of a 64-bit partial sum (chksum_finalize,
+// include/odp_chksum_internal.h)
+__device__ __forceinline__ uint32_t ck_finalize(uint64_t s)
+{
+	s = (s >> 32) + (s & 0xffffffffull);
+	s = (s >> 16) + (s & 0xffffull);
+	return (uint32_t)((s >> 16) + s) & 0xffffu;
+}
+
+// _odp_parse_eth + _odp_packet_parse_common_l3_l4 (layer ALL) with the pktin
+// options `opt` (IPv4 header checksum, drop on IPv4/IPv6/UDP/TCP/SCTP
+// errors; the UDP zero-checksum rule of parse_udp), odp_parse.c:23-105,
+// 112-354, 362-488; contiguous packet so seg_end == frame_len.  The L4
+// checksums themselves are l4_chksum() below.
+__device__ __forceinline__ Parsed parse_packet(const Pkt &k, uint32_t opt)
 {
 	Parsed r;
 	const uint32_t len = k.len;
 	uint32_t f = F_L2 | F_ETH, err = 0, off = 14, ethtype, ip_proto = 255;
 	bool non_first = false;
+	r.udp_zero = 0;
 
 	r.l4 = 0xFFFFu;
 	uint32_t w0 = r32(k, 0), w1 = r32(k, 4);
@@ -197,7 +228,19 @@ __device__ __forceinline__ Parsed parse_packet(const Pkt &k)
 		uint32_t vi = rb(k, l3);
 		uint32_t ihl = vi & 0xfu;
 		uint32_t tot = be16(k, l3 + 2);
-		if (ihl < 5u || (vi >> 4) != 4u || 20u > len - l3 || tot > len - l3) {
+		bool bad = ihl < 5u || (vi >> 4) != 4u || 20u > len - l3 || tot > len - l3;
+		if (!bad && (opt & OPT_IPV4_CK)) {
+			// odp_parse.c:134-141: header checksum over ihl * 4 bytes
+			f |= F_L3CK_DONE;
+			uint64_t s = 0;
+			for (uint32_t i = 0; i < ihl; ++i)
+				s += r32(k, l3 + 4u * i);
+			if (ck_finalize(s) != 0xffffu) {
+				err |= E_L3CK;
+				bad = true;
+			}
+		}
+		if (bad) {
 			err |= E_IP;
 			ip_proto = 0;
 		} else {
@@ -257,6 +300,16 @@ __device__ __forceinline__ Parsed parse_packet(const Pkt &k)
 	} else {
 		f &= ~F_L3;
 	}
+	// drop_ipv4_err / drop_ipv6_err (odp_parse.c:383-387, 392-396): the L4
+	// part is never reached
+	if ((err & E_IP) && (((f & F_IPV4) && (opt & OPT_DROP_V4)) ||
+			     ((f & F_IPV6) && (opt & OPT_DROP_V6)))) {
+		r.l4 = 0xFFFFu;
+		r.flags = f;
+		r.err = err;
+		r.ret = -1;
+		return r;
+	}
 
 	int ret = 0;
 	f |= F_L4;
@@ -274,6 +327,8 @@ __device__ __forceinline__ Parsed parse_packet(const Pkt &k)
 				ret = -1;
 			else if ((rb(k, off + 12) >> 4) < 5u)
 				err |= E_TCP;
+			if ((err & E_TCP) && (opt & OPT_DROP_TCP))
+				ret = -1;
 		}
 		break;
 	case 17u:
@@ -284,11 +339,21 @@ __device__ __forceinline__ Parsed parse_packet(const Pkt &k)
 			} else {
 				uint32_t ports = r32(k, off);
 				uint32_t ulen = be16(k, off + 4);
-				if (ulen < 8u)
+				if (ulen < 8u) {
 					err |= E_UDP;
-				else if ((ports >> 16) == 0x9411u /* be16(4500) raw */ && ulen > 4u &&
-					 r32(k, off + 8) != 0u)
-					f |= F_IPSEC;
+					if (opt & OPT_DROP_UDP)
+						ret = -1;
+				} else {
+					// parse_udp, odp_parse.c:298-313
+					if ((opt & OPT_UDP_CK) && !(f & F_IPFRAG) && r16(k, off + 6) == 0u) {
+						f |= F_L4CK_DONE;
+						err |= (f & F_IPV4) ? 0u : E_L4CK;
+						r.udp_zero = 1;
+					}
+					if ((ports >> 16) == 0x9411u /* be16(4500) raw */ && ulen > 4u &&
+					    r32(k, off + 8) != 0u)
+						f |= F_IPSEC;
+				}
 			}
 		}
 		break;
@@ -305,6 +370,8 @@ __device__ __forceinline__ Parsed parse_packet(const Pkt &k)
 				ret = -1;
 			else if (((len - r.l4) & 0xffffu) < 12u)
 				err |= E_SCTP;
+			if ((err & E_SCTP) && (opt & OPT_DROP_SCTP))
+				ret = -1;
 		}
 		break;
 	case 59u:
@@ -318,6 +385,104 @@ __device__ __forceinline__ Parsed parse_packet(const Pkt &k)
 	r.err = err;
 	r.ret = ret < 0 ? -1 : (err != 0 ? 1 : 0);
 	return r;
+}
+
+// ------------------------------------------------------- pktin checksums
+// CRC-32C (Castagnoli, reflected polynomial 0x82F63B78) byte table, the
+// arithmetic of odp_hash_crc32c (arch/default/odp_hash_crc32.c: table-driven,
+// caller-supplied init, no final inversion).
+struct Crc32cTab {
+	uint32_t v[256];
+	constexpr Crc32cTab() : v()
+	{
+		for (uint32_t i = 0; i < 256; ++i) {
+			uint32_t c = i;
+			for (int b = 0; b < 8; ++b)
+				c = (c & 1u) ? (c >> 1) ^ 0x82F63B78u : (c >> 1);
+			v[i] = c;
+		}
+	}
+};
+__constant__ Crc32cTab c_crc32c;
+
+__device__ __forceinline__ uint32_t crc32c_u8(uint32_t crc, uint32_t b)
+{
+	return c_crc32c.v[(crc ^ b) & 0xffu] ^ (crc >> 8);
+}
+
+// Sum of the little-endian 32-bit words of frame bytes [from, to) (bytes
+// outside are masked to zero), read from HBM in 16-B pieces that start on
+// frame-relative 16-B boundaries, so no piece reaches past the next 16-B
+// boundary after the frame (the batch contract, mi_cls.h).  `from` is even:
+// every 16-bit word of the one's-complement sum stays in one half of a dword.
+__device__ __forceinline__ uint64_t ck_sum_frame(__amdgpu_buffer_rsrc_t rs, uint32_t boff,
+						  uint32_t from, uint32_t to)
+{
+	uint64_t s = 0;
+	for (uint32_t p = from & ~15u; p < to; p += 16u) {
+		const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, boff + p, 0, 0);
+#pragma unroll
+		for (uint32_t j = 0; j < 4; ++j) {
+			const uint32_t q = p + 4u * j;
+			const uint32_t lo = from > q ? min(from - q, 4u) : 0u;
+			const uint32_t hi = to > q ? min(to - q, 4u) : 0u;
+			const uint32_t mhi = hi >= 4u ? ~0u : ((1u << (8u * hi)) - 1u);
+			const uint32_t mlo = lo >= 4u ? ~0u : ((1u << (8u * lo)) - 1u);
+			s += v[j] & mhi & ~mlo;
+		}
+	}
+	return s;
+}
+
+// _odp_packet_l4_chksum (odp_packet.c:2065-2138) for a parse that returned
+// 0, with the partial sums parse_ipv4 / parse_ipv6 / parse_tcp / parse_udp /
+// parse_sctp prepare (odp_parse.c:146-148, 212-214, 267-275, 298-313,
+// 341-351): UDP / TCP one's-complement sum over the pseudo header and
+// [l4, frame_len), SCTP CRC-32C over [l4, frame_len) with the checksum field
+// taken as zero.  Fragments are skipped.  A failure sets l4_chksum_err and
+// the protocol's error bit, and drops the packet under drop_<proto>_err.
+__device__ __forceinline__ void l4_chksum(const Pkt &k, Parsed &p, uint32_t opt,
+					  __amdgpu_buffer_rsrc_t rs, uint32_t boff)
+{
+	if (p.ret != 0 || (p.flags & F_IPFRAG))
+		return;
+	const uint32_t f = p.flags, len = k.len, l3 = p.l3, l4 = p.l4;
+	const uint32_t kind = ((opt & OPT_UDP_CK) && (f & F_UDP) && !p.udp_zero) ? 1u
+		: (((opt & OPT_TCP_CK) && (f & F_TCP)) ? 2u
+		: (((opt & OPT_SCTP_CK) && (f & F_SCTP)) ? 3u : 0u));
+	if (kind == 0u)
+		return;
+	bool bad;
+	if (kind < 3u) {
+		uint64_t s = 0;
+		if (f & F_IPV4) {
+			s = (uint64_t)r32(k, l3 + 12u) + r32(k, l3 + 16u);
+		} else {
+			for (uint32_t i = 0; i < 8u; ++i)
+				s += r32(k, l3 + 8u + 4u * i);
+		}
+		if (kind == 1u)   // udp->length as stored, IPPROTO_UDP << 8
+			s += r16(k, l4 + 4u) + (17u << 8);
+		else              // odp_cpu_to_be_16(frame_len - l4), IPPROTO_TCP << 8
+			s += (((len - l4) & 0xffu) << 8) + (((len - l4) >> 8) & 0xffu) + (6u << 8);
+		s += ck_sum_frame(rs, boff, l4, len);
+		bad = ck_finalize(s) != 0xffffu;   // ~sum != 0
+	} else {
+		uint32_t crc = 0xffffffffu;
+		for (uint32_t i = 0; i < 8u; ++i)
+			crc = crc32c_u8(crc, rb(k, l4 + i));
+		for (uint32_t i = 0; i < 4u; ++i)
+			crc = crc32c_u8(crc, 0u);
+		for (uint32_t o = l4 + 12u; o < len; ++o)
+			crc = crc32c_u8(crc, rb(k, o));
+		bad = ~crc != r32(k, l4 + 8u);
+	}
+	p.flags |= F_L4CK_DONE;
+	if (bad) {
+		p.err |= E_L4CK | (kind == 1u ? E_UDP : (kind == 2u ? E_TCP : E_SCTP));
+		const uint32_t d = kind == 1u ? OPT_DROP_UDP : (kind == 2u ? OPT_DROP_TCP : OPT_DROP_SCTP);
+		p.ret = (opt & d) ? -1 : 1;
+	}
 }
 
 // Branch-light parse for the common header shapes.  Under _odp_parse_eth's
@@ -1053,6 +1218,7 @@ struct KArgs {
 	unsigned long long *stats;   // MAX_STATS_COS counters, or NULL
 	unsigned long long *diag;    // DIAG_STAMPS builds only
 	uint32_t stats_mask[8];
+	uint32_t opt;                // pktin options (OPT_*), 0: none
 };
 
 __device__ __forceinline__ bool stats_bit(const KArgs &a, uint32_t c)
@@ -1063,7 +1229,6 @@ __device__ __forceinline__ bool stats_bit(const KArgs &a, uint32_t c)
 // Buffer offset no frame byte reaches: num_records of the packet resource, so
 // a load at or past it returns zeros (batches are < 4 GiB: u32 offsets).
 #define OOB_OFF 0xFFFFFE00u
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 static_assert(NPIECE == 8 || NPIECE == 6, "WIN must be 96 or 128");
 #define NB (NPIECE - 4)         // upper pieces (phase B)
@@ -1318,11 +1483,20 @@ __global__ __launch_bounds__(NW * WAVE, MIN_WAVES_PER_EU) void mi_cls_kernel(KAr
 		k.len = my_len;
 
 		STAMP(1);   // next tile's loads issued
-		bool slow;
-		Parsed p = parse_fast(k, s_l4, slow);
-		if (__ballot(slow) != 0ull) {
-			if (slow)
-				p = parse_packet(k);
+		Parsed p;
+		if (a.opt == 0u) {
+			bool slow;
+			p = parse_fast(k, s_l4, slow);
+			if (__ballot(slow) != 0ull) {
+				if (slow)
+					p = parse_packet(k, 0u);
+			}
+		} else {
+			// pktin checksum / drop options: the general parser for every
+			// lane, then the L4 checksums (whole frames from HBM)
+			p = parse_packet(k, a.opt);
+			if (a.opt & OPT_L4_CK)
+				l4_chksum(k, p, a.opt, rs, my_off);
 		}
 		const Fields x = fields_of(k, p);
 #ifdef DIAG_PARSEONLY
@@ -1497,6 +1671,7 @@ struct mi_cls_ctx {
 	uint32_t hot_words;      // size of the program's hot region
 	int tree;                // some rule leads to a CoS with rules (DIV kernel)
 	int wpb;                 // forced waves per block (MI_CLS_WPB at load), 0 = auto
+	uint32_t opt;            // pktin options (mi_cls_pktin_opt_set)
 	unsigned long long *d_stats;
 	int stats_on;
 	uint32_t stats_mask[8];
@@ -2194,6 +2369,7 @@ extern "C" int mi_cls_classify(mi_cls_ctx_t *c, const uint8_t *pkts, const uint3
 	a.out = out;
 	a.stats = c->stats_on ? c->d_stats : nullptr;
 	a.diag = nullptr;
+	a.opt = c->opt;
 #ifdef DIAG_STAMPS
 	static unsigned long long *d_diag = nullptr;
 	if (!d_diag)
@@ -2341,6 +2517,16 @@ extern "C" int mi_cls_classify_host(mi_cls_ctx_t *c, const uint8_t *pkts, size_t
 		return rc;
 	HIP_OK(hipMemcpyAsync(out, c->d_out, n * sizeof(mi_cls_result_t), hipMemcpyDeviceToHost, s));
 	HIP_OK(hipStreamSynchronize(s));
+	return 0;
+}
+
+// pktin options for the following classify calls: odp_pktin_config_opt_t
+// all_bits (checksum validation and drop-on-error bits; timestamps ignored).
+extern "C" int mi_cls_pktin_opt_set(mi_cls_ctx_t *c, uint64_t opt)
+{
+	if (!c)
+		return -EINVAL;
+	c->opt = (uint32_t)(opt & 0x7FCull);   // bits 2..10
 	return 0;
 }
 

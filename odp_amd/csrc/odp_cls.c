@@ -84,6 +84,7 @@ typedef struct {
 	void *blob;
 	size_t blob_cap;
 	uint32_t stats_mask[8];
+	uint64_t pktin_opt;      /* odp_pktin_config_opt_t.all_bits */
 } pktio_t;
 
 static struct {
@@ -976,8 +977,21 @@ int odp_amd_cls_classify(odp_pktio_t h, const uint8_t *pkts_dev, const uint32_t 
 	rc = sync_rules(e, stream);
 	if (rc)
 		return rc;
+	mi_cls_pktin_opt_set(e->ctx, e->pktin_opt);
 	return mi_cls_classify(e->ctx, pkts_dev, off_dev, len_dev, n, (mi_cls_result_t *)out_dev,
 			       stream);
+}
+
+/* The pktio's pktin parse options (odp_pktio_config() -> config.pktin,
+ * used by the receive path as _odp_packet_parse_common's `opt`). */
+int odp_amd_cls_pktin_opt_set(odp_pktio_t h, uint64_t opt)
+{
+	pktio_t *e = get_pktio(h);
+
+	if (!e)
+		return -EINVAL;
+	e->pktin_opt = opt;
+	return 0;
 }
 
 odp_queue_t odp_amd_cls_queue_of(uint32_t cos_index, uint32_t slot)
@@ -1244,6 +1258,7 @@ int odp_amd_cls_classify_host(odp_pktio_t h, const uint8_t *pkts, size_t bytes,
 		rc = ensure_parse_ctx(e);
 		if (rc)
 			return rc;
+		mi_cls_pktin_opt_set(e->pctx, e->pktin_opt);
 		return mi_cls_classify_host(e->pctx, pkts, bytes, off, len, n,
 					    (mi_cls_result_t *)out);
 	}
@@ -1253,6 +1268,7 @@ int odp_amd_cls_classify_host(odp_pktio_t h, const uint8_t *pkts, size_t bytes,
 	rc = sync_rules(e, NULL);
 	if (rc)
 		return rc;
+	mi_cls_pktin_opt_set(e->ctx, e->pktin_opt);
 	return mi_cls_classify_host(e->ctx, pkts, bytes, off, len, n, (mi_cls_result_t *)out);
 }
 

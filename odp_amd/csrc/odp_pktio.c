@@ -495,6 +495,7 @@ int odp_pktio_capability(odp_pktio_t h, odp_pktio_capability_t *c)
 	c->max_output_queue_size = 0;
 	odp_pktio_config_init(&c->config);
 	c->config.parser.layer = ODP_PROTO_LAYER_ALL;
+	c->config.pktin.all_bits = RT_PKTIN_OPT_MASK;
 	c->config.enable_loop = 0;
 	c->set_op.op.promisc_mode = e->drv == DRV_PCAP;
 	c->maxlen.equal = 1;
@@ -515,9 +516,11 @@ int odp_pktio_config(odp_pktio_t h, const odp_pktio_config_t *config)
 		odp_pktio_config_init(&def);
 		config = &def;
 	}
-	/* only parser options and the zero checksum/ts options are supported */
-	if (config->pktin.all_bits || config->pktout.all_bits || config->enable_loop ||
-	    config->inbound_ipsec || config->outbound_ipsec || config->enable_lso) {
+	/* parser options, pktin checksum validation and drop-on-error options
+	 * (bits 2-10); no timestamps, pktout offloads, IPsec or LSO */
+	if ((config->pktin.all_bits & ~RT_PKTIN_OPT_MASK) || config->pktout.all_bits ||
+	    config->enable_loop || config->inbound_ipsec || config->outbound_ipsec ||
+	    config->enable_lso) {
 		RT_ERR("pktio %s: unsupported configuration option\n", e->name);
 		return -1;
 	}
@@ -646,6 +649,16 @@ int odp_pktio_start(odp_pktio_t h)
 	e->parse_layer = e->cls_enabled ? ODP_PROTO_LAYER_ALL : e->config.parser.layer;
 	/* GPU context, rule snapshot and a warm-up launch before traffic */
 	if (e->param.in_mode != ODP_PKTIN_MODE_DISABLED && e->parse_layer != ODP_PROTO_LAYER_NONE) {
+		/* the options of the layers that are parsed: L3 takes the IPv4
+		 * header checksum and the IP drops, L4 everything (odp_parse.c:
+		 * 372-414 stop before the rest) */
+		uint64_t opt = e->config.pktin.all_bits & RT_PKTIN_OPT_MASK;
+
+		if (e->parse_layer < ODP_PROTO_LAYER_L3)
+			opt = 0;
+		else if (e->parse_layer == ODP_PROTO_LAYER_L3)
+			opt &= (1u << 2) | (1u << 6) | (1u << 7);
+		odp_amd_cls_pktin_opt_set(h, opt);
 		int rc = odp_amd_cls_prepare(h, !e->cls_enabled);
 
 		if (rc) {
@@ -800,15 +813,17 @@ static void apply_layer(mi_cls_result_t *r, odp_proto_layer_t layer)
 
 	if (layer >= ODP_PROTO_LAYER_L4)
 		return;
-	if (r->outcome == MI_CLS_OUT_PARSE_DROP)
+	/* an L4 truncation does not drop below L4; a drop_ipv4/6_err drop
+	 * (ip_err set, L3 options) does */
+	if (r->outcome == MI_CLS_OUT_PARSE_DROP && !(layer == ODP_PROTO_LAYER_L3 && (r->err & 0x02)))
 		r->outcome = MI_CLS_OUT_DISCARD;
 	if (layer == ODP_PROTO_LAYER_L2) {
 		r->in_flags &= L2F;
 		r->err &= 0x01;     /* snap_len_err */
 		r->l4_offset = ODP_PACKET_OFFSET_INVALID;
 	} else {
-		r->in_flags &= L3F;
-		r->err &= 0x03;     /* snap_len_err, ip_err */
+		r->in_flags &= L3F | (1u << 30);   /* + l3_chksum_done */
+		r->err &= 0x07;     /* snap_len_err, ip_err, l3_chksum_err */
 	}
 }
 

@@ -993,6 +993,26 @@ int odp_packet_has_l2_error(odp_packet_t pkt) { return (rt_pkt_hdr(pkt)->err & 0
 int odp_packet_has_l3_error(odp_packet_t pkt) { return (rt_pkt_hdr(pkt)->err & 0x06) != 0; }
 int odp_packet_has_l4_error(odp_packet_t pkt) { return (rt_pkt_hdr(pkt)->err & 0x78) != 0; }
 
+/* packet_inlines.h:389-420: input_flags l3/l4_chksum_done (bits 30/31),
+ * error bits l3_chksum_err (2) / l4_chksum_err (6) */
+odp_packet_chksum_status_t odp_packet_l3_chksum_status(odp_packet_t pkt)
+{
+	const pkt_hdr_t *h = rt_pkt_hdr(pkt);
+
+	if (!((h->in_flags >> 30) & 1u))
+		return ODP_PACKET_CHKSUM_UNKNOWN;
+	return (h->err & 0x04) ? ODP_PACKET_CHKSUM_BAD : ODP_PACKET_CHKSUM_OK;
+}
+
+odp_packet_chksum_status_t odp_packet_l4_chksum_status(odp_packet_t pkt)
+{
+	const pkt_hdr_t *h = rt_pkt_hdr(pkt);
+
+	if (!((h->in_flags >> 31) & 1u))
+		return ODP_PACKET_CHKSUM_UNKNOWN;
+	return (h->err & 0x40) ? ODP_PACKET_CHKSUM_BAD : ODP_PACKET_CHKSUM_OK;
+}
+
 /* accessor for odp_cls_hash_result (odp_cls.c) */
 int _odp_amd_packet_parse_info(odp_packet_t pkt, const uint8_t **data, uint64_t *in_flags,
 			       uint32_t *l3, uint32_t *l4)

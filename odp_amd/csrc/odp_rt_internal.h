@@ -15,6 +15,9 @@
 #define RT_MAX_PKTIO   64
 #define RT_MAX_AGGR    4
 /* CONFIG_PACKET_HEADROOM (platform/linux-generic/include/odp_config_internal.h:105) */
+/* odp_pktin_config_opt_t bits the receive path implements: ipv4/udp/tcp/
+ * sctp checksum validation and the five drop-on-error options */
+#define RT_PKTIN_OPT_MASK 0x7FCull
 #define RT_PKT_HEADROOM 128
 #define RT_PKT_TAILROOM 64
 

@@ -176,8 +176,73 @@ error:
 	return ethtype;
 }
 
-/* parse_ipv4, odp_parse.c:112-173 (checksum options off) */
-static uint32_t parse_ipv4(orc_parser_t *prs, const pkt_t *k, uint32_t *offset, int *non_first)
+/* ------------------------------------------------------ pktin options */
+/* odp_pktin_config_opt_t.all_bits (include/odp/api/spec/packet_io.h) */
+#define O_IPV4_CK    (1ull << 2)
+#define O_UDP_CK     (1ull << 3)
+#define O_TCP_CK     (1ull << 4)
+#define O_SCTP_CK    (1ull << 5)
+#define O_DROP_V4    (1ull << 6)
+#define O_DROP_V6    (1ull << 7)
+#define O_DROP_UDP   (1ull << 8)
+#define O_DROP_TCP   (1ull << 9)
+#define O_DROP_SCTP  (1ull << 10)
+#define IF_L3_CHKSUM_DONE  (1ull << 30)
+#define IF_L4_CHKSUM_DONE  (1ull << 31)
+#define IF_UDP_CHKSUM_ZERO (1ull << 32)
+
+static uint64_t g_opt;   /* pktio_entry->config.pktin of the receive path */
+
+void orc_pktin_opt_set(uint64_t opt)
+{
+	g_opt = opt;
+}
+
+/* chksum_partial, include/odp_chksum_internal.h (the unaligned-access form;
+ * every caller here starts at an even offset from L3): 32-bit little-endian
+ * words, then a 16-bit word, then a last byte as the low byte. */
+static uint64_t chksum_partial(const pkt_t *k, uint32_t o, uint32_t len)
+{
+	uint64_t sum = 0;
+
+	while (len >= 4) {
+		sum += raw32(k, o);
+		o += 4;
+		len -= 4;
+	}
+	if (len > 1) {
+		sum += raw16(k, o);
+		o += 2;
+		len -= 2;
+	}
+	if (len)
+		sum += B(k, o);   /* odp_cpu_to_be_16(b << 8) on a little-endian CPU */
+	return sum;
+}
+
+/* chksum_finalize, include/odp_chksum_internal.h */
+static uint16_t chksum_finalize(uint64_t sum)
+{
+	sum = (sum >> 32) + (sum & 0xffffffff);
+	sum = (sum >> 16) + (sum & 0xffff);
+	return (uint16_t)((sum >> 16) + sum);
+}
+
+/* odp_hash_crc32c (arch/default/odp_hash_crc32.c): reflected CRC-32C,
+ * caller-supplied init, no final inversion; byte at a time. */
+static uint32_t crc32c_bytes(uint32_t crc, const pkt_t *k, uint32_t o, uint32_t len)
+{
+	for (uint32_t i = 0; i < len; i++) {
+		crc ^= B(k, o + i);
+		for (int b = 0; b < 8; b++)
+			crc = (crc & 1) ? (crc >> 1) ^ 0x82F63B78u : crc >> 1;
+	}
+	return crc;
+}
+
+/* parse_ipv4, odp_parse.c:112-173 */
+static uint32_t parse_ipv4(orc_parser_t *prs, const pkt_t *k, uint32_t *offset, int *non_first,
+			   uint64_t *l4_part_sum)
 {
 	uint32_t o = *offset, frame_len = k->len;
 	uint32_t dst = be32(k, o + 16);
@@ -185,11 +250,21 @@ static uint32_t parse_ipv4(orc_parser_t *prs, const pkt_t *k, uint32_t *offset, 
 	uint32_t frag = be16(k, o + 6);
 	uint32_t ver = B(k, o) >> 4, ihl = B(k, o) & 0xf;
 
-	if (ihl < 5 || ver != 4 || 20 > frame_len - o || l3_len > frame_len - o) {
+	if ((prs->err & ER_L3_CHKSUM) || ihl < 5 || ver != 4 || 20 > frame_len - o ||
+	    l3_len > frame_len - o) {
 		prs->err |= ER_IP;
 		return 0;
 	}
+	if (g_opt & O_IPV4_CK) {
+		prs->input_flags |= IF_L3_CHKSUM_DONE;
+		if (chksum_finalize(chksum_partial(k, o, ihl * 4)) != 0xffff) {
+			prs->err |= ER_IP | ER_L3_CHKSUM;
+			return 0;
+		}
+	}
 	*offset += ihl * 4;
+	if (g_opt & (O_UDP_CK | O_TCP_CK))
+		*l4_part_sum = chksum_partial(k, o + 12, 8);   /* src + dst address */
 	if (ihl > 5)
 		prs->input_flags |= IF_IPOPT;
 	if (frag & 0x3fff) {
@@ -205,14 +280,16 @@ static uint32_t parse_ipv4(orc_parser_t *prs, const pkt_t *k, uint32_t *offset, 
 }
 
 /* parse_ipv6, odp_parse.c:183-249 */
-static uint32_t parse_ipv6(orc_parser_t *prs, const pkt_t *k, uint32_t *offset, uint32_t seg_end)
+static uint32_t parse_ipv6(orc_parser_t *prs, const pkt_t *k, uint32_t *offset, uint32_t seg_end,
+			   uint64_t *l4_part_sum)
 {
 	uint32_t o = *offset, frame_len = k->len;
 	uint32_t dst0 = be32(k, o + 24);
 	uint32_t plen = be16(k, o + 4);
 	uint32_t l3_len = plen + 40;
 
-	if ((be32(k, o) >> 28) != 6 || 40 > frame_len - o || l3_len > frame_len - o) {
+	if ((prs->err & ER_L3_CHKSUM) || (be32(k, o) >> 28) != 6 || 40 > frame_len - o ||
+	    l3_len > frame_len - o) {
 		prs->err |= ER_IP;
 		return 0;
 	}
@@ -223,6 +300,8 @@ static uint32_t parse_ipv6(orc_parser_t *prs, const pkt_t *k, uint32_t *offset, 
 	prs->input_flags &= ~IF_IP_BCAST;
 
 	*offset += 40;
+	if (g_opt & (O_UDP_CK | O_TCP_CK))
+		*l4_part_sum = chksum_partial(k, o + 8, 32);   /* src + dst address */
 	uint32_t nh = B(k, o + 6);
 	if (nh == 0 || nh == 43) {
 		uint32_t ext, nxt;
@@ -247,19 +326,77 @@ static uint32_t parse_ipv6(orc_parser_t *prs, const pkt_t *k, uint32_t *offset, 
 	return nh;
 }
 
-/* packet_parse_reset(all=1) + _odp_packet_parse_common (layer ALL, opt 0):
+/* _odp_packet_l4_chksum, odp_packet.c:2065-2138 (contiguous packet:
+ * packet_sum over [l4, frame_len) from the even offset l4 - l3). */
+static int l4_chksum(const pkt_t *k, orc_parser_t *prs, uint64_t l4_part_sum)
+{
+	uint32_t frame_len = k->len, l4 = prs->l4;
+
+	if (prs->input_flags & IF_IPFRAG)
+		return prs->err != 0;
+	if ((g_opt & O_UDP_CK) && (prs->input_flags & IF_UDP) &&
+	    !(prs->input_flags & IF_UDP_CHKSUM_ZERO)) {
+		uint16_t sum = (uint16_t)~chksum_finalize(l4_part_sum +
+							  chksum_partial(k, l4, frame_len - l4));
+
+		prs->input_flags |= IF_L4_CHKSUM_DONE;
+		if (sum != 0) {
+			prs->err |= ER_L4_CHKSUM | ER_UDP;
+			if (g_opt & O_DROP_UDP)
+				return -1;
+		}
+	} else if ((g_opt & O_TCP_CK) && (prs->input_flags & IF_TCP)) {
+		uint16_t sum = (uint16_t)~chksum_finalize(l4_part_sum +
+							  chksum_partial(k, l4, frame_len - l4));
+
+		prs->input_flags |= IF_L4_CHKSUM_DONE;
+		if (sum != 0) {
+			prs->err |= ER_L4_CHKSUM | ER_TCP;
+			if (g_opt & O_DROP_TCP)
+				return -1;
+		}
+	} else if ((g_opt & O_SCTP_CK) && (prs->input_flags & IF_SCTP)) {
+		uint32_t sum = ~crc32c_bytes((uint32_t)l4_part_sum, k, l4 + 12, frame_len - l4 - 12);
+
+		prs->input_flags |= IF_L4_CHKSUM_DONE;
+		if (sum != raw32(k, l4 + 8)) {
+			prs->err |= ER_L4_CHKSUM | ER_SCTP;
+			if (g_opt & O_DROP_SCTP)
+				return -1;
+		}
+	}
+	return prs->err != 0;
+}
+
+/* packet_parse_reset(all=1) + _odp_packet_parse_common (layer ALL, the
+ * pktin options set by orc_pktin_opt_set):
  * odp_packet_internal.h:468-479, odp_parse_internal.h:80-112,
  * odp_parse.c:362-488.  Returns 0 ok, 1 error flags set, -1 drop. */
+static int parse_l3_l4(const pkt_t *kp, orc_parser_t *prs, uint64_t *l4_part_sum);
+
 int orc_parse(const uint8_t *p, uint32_t frame_len, orc_parser_t *prs)
 {
 	pkt_t k = { p, frame_len };
-	uint32_t seg_end = frame_len;   /* contiguous packet: seg_len == frame_len */
-	uint32_t offset = 0, ip_proto = 255, ethtype;
-	int non_first = 0;
+	uint64_t l4_part_sum = 0;
+	int r;
 
 	prs->input_flags = 0;
 	prs->err = 0;
 	prs->l2 = prs->l3 = prs->l4 = 0xFFFF;
+	r = parse_l3_l4(&k, prs, &l4_part_sum);
+	if (!r && (g_opt & (O_UDP_CK | O_TCP_CK | O_SCTP_CK)))
+		r = l4_chksum(&k, prs, l4_part_sum);
+	prs->input_flags &= ~IF_UDP_CHKSUM_ZERO;   /* internal: not in the record */
+	return r;
+}
+
+static int parse_l3_l4(const pkt_t *kp, orc_parser_t *prs, uint64_t *l4_part_sum)
+{
+	pkt_t k = *kp;
+	uint32_t frame_len = k.len;
+	uint32_t seg_end = frame_len;   /* contiguous packet: seg_len == frame_len */
+	uint32_t offset = 0, ip_proto = 255, ethtype;
+	int non_first = 0;
 
 	prs->l2 = 0;
 	ethtype = parse_eth(prs, &k, &offset);
@@ -269,15 +406,19 @@ int orc_parse(const uint8_t *p, uint32_t frame_len, orc_parser_t *prs)
 	switch (ethtype) {
 	case 0x0800:
 		prs->input_flags |= IF_IPV4;
-		ip_proto = parse_ipv4(prs, &k, &offset, &non_first);
+		ip_proto = parse_ipv4(prs, &k, &offset, &non_first, l4_part_sum);
 		if (!(prs->err & ER_IP))
 			prs->l4 = (uint16_t)offset;
+		else if (g_opt & O_DROP_V4)
+			return -1;
 		break;
 	case 0x86DD:
 		prs->input_flags |= IF_IPV6;
-		ip_proto = parse_ipv6(prs, &k, &offset, seg_end);
+		ip_proto = parse_ipv6(prs, &k, &offset, seg_end, l4_part_sum);
 		if (!(prs->err & ER_IP))
 			prs->l4 = (uint16_t)offset;
+		else if (g_opt & O_DROP_V6)
+			return -1;
 		break;
 	case 0x0806:
 		prs->input_flags |= IF_ARP;
@@ -302,8 +443,17 @@ int orc_parse(const uint8_t *p, uint32_t frame_len, orc_parser_t *prs)
 			return prs->err != 0;
 		if (offset + 20 > seg_end)
 			return -1;
+		/* parse_tcp, odp_parse.c:256-278 */
 		if ((B(&k, offset + 12) >> 4) < 5)
 			prs->err |= ER_TCP;
+		if ((g_opt & O_TCP_CK) && !(prs->input_flags & IF_IPFRAG)) {
+			uint16_t tcp_len = (uint16_t)(frame_len - prs->l4);
+
+			*l4_part_sum += (uint16_t)((tcp_len >> 8) | (tcp_len << 8));   /* cpu_to_be_16 */
+			*l4_part_sum += 6 << 8;
+		}
+		if ((prs->err & ER_TCP) && (g_opt & O_DROP_TCP))
+			return -1;
 		break;
 	case 17:
 		prs->input_flags |= IF_UDP;
@@ -311,17 +461,31 @@ int orc_parse(const uint8_t *p, uint32_t frame_len, orc_parser_t *prs)
 			return prs->err != 0;
 		if (offset + 8 > seg_end)
 			return -1;
+		/* parse_udp, odp_parse.c:285-327 */
 		{
 			uint32_t udplen = be16(&k, offset + 4);
 
 			if (udplen < 8) {
 				prs->err |= ER_UDP;
-				break;
+			} else {
+				if ((g_opt & O_UDP_CK) && !(prs->input_flags & IF_IPFRAG)) {
+					if (raw16(&k, offset + 6) == 0) {
+						prs->input_flags |= IF_L4_CHKSUM_DONE;
+						if (!(prs->input_flags & IF_IPV4))
+							prs->err |= ER_L4_CHKSUM;
+						prs->input_flags |= IF_UDP_CHKSUM_ZERO;
+					} else {
+						*l4_part_sum += raw16(&k, offset + 4);   /* udp->length */
+						*l4_part_sum += 17 << 8;
+					}
+				}
+				if (be16(&k, offset + 2) == 4500 && udplen > 4 &&
+				    raw32(&k, offset + 8) != 0)
+					prs->input_flags |= IF_IPSEC;
 			}
-			if (be16(&k, offset + 2) == 4500 && udplen > 4 &&
-			    raw32(&k, offset + 8) != 0)
-				prs->input_flags |= IF_IPSEC;
 		}
+		if ((prs->err & ER_UDP) && (g_opt & O_DROP_UDP))
+			return -1;
 		break;
 	case 51:
 		prs->input_flags |= IF_IPSEC | IF_IPSEC_AH;
@@ -335,8 +499,18 @@ int orc_parse(const uint8_t *p, uint32_t frame_len, orc_parser_t *prs)
 			return prs->err != 0;
 		if (offset + 12 > seg_end)
 			return -1;
-		if ((uint16_t)(frame_len - prs->l4) < 12)
+		/* parse_sctp, odp_parse.c:334-356 */
+		if ((uint16_t)(frame_len - prs->l4) < 12) {
 			prs->err |= ER_SCTP;
+		} else if ((g_opt & O_SCTP_CK) && !(prs->input_flags & IF_IPFRAG)) {
+			uint32_t crc = crc32c_bytes(~0u, &k, offset, 8);
+			static const uint8_t zero4[4];
+			pkt_t z = { zero4, 4 };
+
+			*l4_part_sum = crc32c_bytes(crc, &z, 0, 4);
+		}
+		if ((prs->err & ER_SCTP) && (g_opt & O_DROP_SCTP))
+			return -1;
 		break;
 	case 59:
 		prs->input_flags |= IF_NO_NEXT;
@@ -345,7 +519,6 @@ int orc_parse(const uint8_t *p, uint32_t frame_len, orc_parser_t *prs)
 		prs->input_flags &= ~IF_L4;
 		break;
 	}
-	/* _odp_packet_l4_chksum with all checksum options off (odp_packet.c:2065) */
 	return prs->err != 0;
 }
 

@@ -64,6 +64,8 @@ def lib():
         L.orc_rss_hash_one.restype = u32
         L.orc_softrss.argtypes = [C.POINTER(C.c_uint32), u32]
         L.orc_softrss.restype = u32
+        L.orc_pktin_opt_set.argtypes = [C.c_uint64]
+        L.orc_pktin_opt_set.restype = None
         _lib = L
     return _lib
 
@@ -71,12 +73,14 @@ def lib():
 class Oracle:
     """Scalar model of linux-generic's classifier tables + data path."""
 
-    def __init__(self, limits=(255, 8192, 4096), max_hops=None):
+    def __init__(self, limits=(255, 8192, 4096), max_hops=None, pktin_opt=0):
         self.L = lib()
         self.L.orc_reset(*limits)
         self.max_hops = limits[0] if max_hops is None else max_hops
         self.cos = []
         self.pmr = []
+        # odp_pktin_config_opt_t.all_bits (checksum validation / drop on error)
+        self.pktin_opt = pktin_opt
 
     def cos_create(self, action=0, queue=1, num_queue=1, hash_proto=0, stats=0):
         return self.L.orc_cos_create(action, num_queue, 1 if queue else 0, hash_proto, stats)
@@ -120,6 +124,7 @@ class Oracle:
         buf = np.ascontiguousarray(batch.buf)
         off = np.ascontiguousarray(batch.off, dtype=np.uint32)
         ln = np.ascontiguousarray(batch.len, dtype=np.uint16)
+        self.L.orc_pktin_opt_set(self.pktin_opt)
         if threads == 1:
             self.L.orc_classify_batch(buf.ctypes.data, off.ctypes.data, ln.ctypes.data, n,
                                       out.ctypes.data, self.max_hops)
@@ -132,9 +137,10 @@ class Oracle:
         return self.L.orc_cos_stats_packets(cos_handle)
 
 
-def parse(frame: bytes):
+def parse(frame: bytes, pktin_opt=0):
     """Parse one frame; returns (ret, input_flags, err, l2, l3, l4)."""
     L = lib()
+    L.orc_pktin_opt_set(pktin_opt)
     b = np.frombuffer(frame + bytes(8), dtype=np.uint8)
     f, e = C.c_uint64(), C.c_uint32()
     l2, l3, l4 = C.c_uint16(), C.c_uint16(), C.c_uint16()

@@ -5,18 +5,20 @@ import numpy as np
 from odp_amd import rules as R
 
 
-def oracle_run(prog, batch, limits=(255, 8192, 4096)):
+def oracle_run(prog, batch, limits=(255, 8192, 4096), pktin_opt=0):
     from oracle.oracle import Oracle
-    o = Oracle(limits=limits)
+    o = Oracle(limits=limits, pktin_opt=pktin_opt)
     o.apply(prog)
     return o.classify(batch), o
 
 
-def gpu_run(prog, batch, limits=(255, 8192, 4096)):
+def gpu_run(prog, batch, limits=(255, 8192, 4096), pktin_opt=0):
     from odp_amd.cls import Classifier
     c = Classifier(gpu=0, limits=limits)
     try:
         c.apply(prog)
+        if pktin_opt:
+            c.set_pktin_opt(pktin_opt)
         return c.classify(batch)
     finally:
         c.close()

@@ -182,6 +182,9 @@ static void print_pkt(const char *q, odp_packet_t pkt)
 	for (unsigned b = 0; b < sizeof(fn) / sizeof(fn[0]); b++)
 		if (fn[b] && fn[b](pkt))
 			fl |= 1ull << b;
+	/* checksum statuses (0 unknown, 1 bad, 2 ok) in bits 40-41 / 42-43 */
+	fl |= (uint64_t)odp_packet_l3_chksum_status(pkt) << 40;
+	fl |= (uint64_t)odp_packet_l4_chksum_status(pkt) << 42;
 	printf("P %s %s %" PRIx64 " %d %u %u %" PRIu64 " %u ", q, poolname(odp_packet_pool(pkt)), fl,
 	       odp_packet_has_error(pkt), odp_packet_l3_offset(pkt), odp_packet_l4_offset(pkt),
 	       odp_packet_cls_mark(pkt), len);
@@ -232,6 +235,9 @@ int main(int argc, char *argv[])
 		odp_pktio_promisc_mode_set(pktio, 1);
 	odp_pktio_config_init(&cfg);
 	cfg.parser.layer = (odp_proto_layer_t)layer;
+	/* RX_PKTIN_OPT: odp_pktin_config_opt_t.all_bits (checksum / drop options) */
+	if (getenv("RX_PKTIN_OPT"))
+		cfg.pktin.all_bits = strtoull(getenv("RX_PKTIN_OPT"), NULL, 0);
 	if (odp_pktio_config(pktio, &cfg))
 		return 6;
 	if (strcmp(argv[2], "-") != 0) {

@@ -119,11 +119,20 @@ def cos_names(prog):
     return slots
 
 
-def expected(prog, frames, cos_pools=1, cls=1, layer=4, pktin_queue="odp-pktin-0-0"):
+def expected(prog, frames, cos_pools=1, cls=1, layer=4, pktin_queue="odp-pktin-0-0",
+             pktin_opt=0):
     """Per-queue packet sequences and pktio stats the reference receive path
-    produces, from the oracle's per-frame records."""
+    produces, from the oracle's per-frame records.  pktin_opt: the pktio's
+    odp_pktin_config_opt_t bits (the L3 layer takes only the IPv4 checksum
+    and the IP drops, L2 none: odp_parse.c:372-414 stop before the rest)."""
     from oracle.oracle import Oracle
-    o = Oracle()
+    if cls:
+        layer = 4   # the classifier parses every layer (odp_packet_io.c:675-677)
+    if layer == 2:
+        pktin_opt &= (1 << 2) | (1 << 6) | (1 << 7)
+    elif layer < 2:
+        pktin_opt = 0
+    o = Oracle(pktin_opt=pktin_opt)
     o.apply(prog if cls else [])
     recs = o.classify(pg.batch_from_frames(frames))
     slots = cos_names(prog) if cls else {}
@@ -131,19 +140,19 @@ def expected(prog, frames, cos_pools=1, cls=1, layer=4, pktin_queue="odp-pktin-0
     qstats = defaultdict(lambda: [0, 0])
     in_pk = in_err = in_disc = octets = 0
     l2m = (1 << 3) | (0x3f << 6)
-    l3m = l2m | (1 << 4) | (0x7f << 12)
+    l3m = l2m | (1 << 4) | (0x7f << 12) | (1 << 30)
     for fr, r in zip(frames, recs):
         fl, err, out = int(r["in_flags"]), int(r["err"]), int(r["outcome"])
         l3, l4 = int(r["l3_offset"]), int(r["l4_offset"])
         if layer == 0:
             fl, err, l3, l4 = 0, 0, 0xFFFF, 0xFFFF
         elif layer < 3:     # L2 (1) and L3 (2) cut the parse (odp_parse.c:372-414)
-            if out == R.OUT_PARSE_DROP:
+            if out == R.OUT_PARSE_DROP and not (layer == 2 and err & 2):
                 out = R.OUT_DISCARD
             if layer == 1:
                 fl, err, l4 = fl & l2m, err & 1, 0xFFFF
             else:
-                fl, err = fl & l3m, err & 3
+                fl, err = fl & l3m, err & 7
         if layer and (err or out == R.OUT_PARSE_DROP):
             in_err += 1
         if layer and out == R.OUT_PARSE_DROP:
@@ -165,7 +174,11 @@ def expected(prog, frames, cos_pools=1, cls=1, layer=4, pktin_queue="odp-pktin-0
             in_pk += 1
             octets += len(fr)
         mark = int(r["mark"]) if (fl & 1) else 0
-        queues[q].append((pool, fl & FLAG_MASK, int(err != 0), l3, l4, mark, len(fr), fr.hex()))
+        # checksum statuses as the driver reports them (0 unknown, 1 bad, 2 ok)
+        l3st = 0 if not (fl >> 30) & 1 else (1 if err & 4 else 2)
+        l4st = 0 if not (fl >> 31) & 1 else (1 if err & 64 else 2)
+        fl_rep = (fl & FLAG_MASK) | (l3st << 40) | (l4st << 42)
+        queues[q].append((pool, fl_rep, int(err != 0), l3, l4, mark, len(fr), fr.hex()))
     return dict(queues), (in_pk, in_err, in_disc, octets), dict(qstats)
 
 

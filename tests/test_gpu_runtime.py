@@ -25,17 +25,19 @@ UDP64 = os.path.join(H.ROOT, "tests", "golden", "udp64.pcap")
 
 
 def _run_case(tmp_path, prog, frames, mode="sched", pktio="pcap", cos_pools=1, layer=4, cls=1,
-              burst=None):
+              burst=None, pktin_opt=0):
     pc = str(tmp_path / "in.pcap")
     H.write_pcap(pc, frames)
     rules = str(tmp_path / "rules.txt")
     H.write_rules(rules, prog)
-    env = {"ODP_AMD_RX_BURST": str(burst)} if burst else None
+    env = {"ODP_AMD_RX_BURST": str(burst)} if burst else {}
+    if pktin_opt:
+        env["RX_PKTIN_OPT"] = str(pktin_opt)
     if pktio == "loop":
         got = H.run_driver("loop", rules, mode, layer, cos_pools, cls, src=pc, env=env)
     else:
         got = H.run_driver(f"pcap:in={pc}", rules, mode, layer, cos_pools, cls, env=env)
-    exp = H.expected(prog, frames, cos_pools, cls, layer)
+    exp = H.expected(prog, frames, cos_pools, cls, layer, pktin_opt=pktin_opt)
     H.compare(got, exp)
     return got
 
@@ -113,6 +115,19 @@ def test_rx_random_programs_small_bursts(built, gpu, tmp_path):
         if any(op[0] == "cos" and " " in op[1] for op in prog):
             continue
         _run_case(tmp_path, prog, frames, burst=37)
+
+
+@pytest.mark.parametrize("layer,opt,cls", [(4, 0x3C, 1), (4, 0x7FC, 1), (4, 0x780, 1),
+                                           (2, 0x7FC, 0), (3, 0x7FC, 0), (4, 0x7FC, 0)])
+def test_rx_pktin_checksum_options(built, gpu, tmp_path, layer, opt, cls):
+    """odp_pktio_config(pktin.bit.*_chksum / drop_*_err) through the runtime:
+    checksum statuses (odp_packet_l3/l4_chksum_status), error-CoS routing,
+    drops and in_errors as the reference receive path produces them; with the
+    classifier off, the parser layer limits which options apply."""
+    from tests import chksum_frames as CK
+    frames = H.pcap_frames([f for f, _, _ in CK.frame_set(seed=51, n=120)] +
+                           [f for _, f in zoo.all_frames()])
+    _run_case(tmp_path, zoo.prog_everything(), frames, layer=layer, cls=cls, pktin_opt=opt)
 
 
 def test_rx_config2_traffic(built, gpu, tmp_path):
