@@ -312,6 +312,27 @@ def main():
                         "mpkts_per_s": round(b2.n * k_steps / w2 / 1e6, 2),
                         "kernel_ms": round(k2, 4), "roofline_frac": round(ach / HBM_PEAK_GBS, 5),
                         "rules": R.rule_count(p2)}
+                # pktin checksum validation (IPv4 header, UDP/TCP sums over the
+                # whole frame): config 3 IMIX with valid checksums; the kernel
+                # reads every frame byte, so the bytes are frame + 22 B
+                from odp_amd import pktgen as pg
+                b2, p2 = make_workload(3, a.n, 0)
+                pg.set_checksums(b2)
+                c2 = cls.Classifier(gpu=local)
+                c2.apply(p2)
+                c2.set_pktin_opt(0x3C)
+                k_steps = max(5, a.steps // 5)
+                w2, _, _ = time_device(c2, b2, dev, k_steps, 3, rotate=a.rotate,
+                                       streams=a.streams)
+                _, k2, _ = time_device(c2, b2, dev, k_steps, 3, rotate=a.rotate)
+                c2.close()
+                fb = int(b2.len.astype(np.int64).sum()) + 22 * b2.n
+                extra["config3_imix_256rules_checksums"] = {
+                    "mpkts_per_s": round(b2.n * k_steps / w2 / 1e6, 2),
+                    "kernel_ms": round(k2, 4),
+                    "roofline_frac": round(fb / (k2 * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+                    "bytes_per_launch": fb, "pktin_opt": "ipv4/udp/tcp/sctp checksums",
+                    "rules": R.rule_count(p2)}
                 line["extra"] = extra
         res = line
         print(json.dumps(res), flush=True)

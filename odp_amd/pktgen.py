@@ -319,6 +319,53 @@ def build_batch(lens, *, ipver, l4proto, sip4=None, dip4=None, sip6=None, dip6=N
     return Batch(buf, off.astype(np.uint32), lens.astype(np.uint16))
 
 
+def set_checksums(b: Batch, l3: int = 14) -> Batch:
+    """Write valid IPv4 header and UDP / TCP checksums (RFC 1071 sums, RFC 768
+    / 793 / 8200 pseudo headers) into an untagged build_batch() batch (IPv4
+    IHL 5 or IPv6 without extension headers), in place, vectorised."""
+    buf = b.buf
+    off = b.off.astype(np.int64)
+    ln = b.len.astype(np.int64)
+
+    def fold(s):
+        s = (s & 0xFFFF) + (s >> 16)
+        s = (s & 0xFFFF) + (s >> 16)
+        return (s & 0xFFFF) + (s >> 16)
+
+    def words(base, nw):
+        idx = base[:, None] + 2 * np.arange(nw)[None, :]
+        return ((buf[idx].astype(np.int64) << 8) | buf[idx + 1]).sum(1)
+
+    et = (buf[off + 12].astype(np.int64) << 8) | buf[off + 13]
+    v4 = et == ETH_IPV4
+    o4 = off[v4] + l3
+    buf[o4 + 10] = 0
+    buf[o4 + 11] = 0
+    c = ~fold(words(o4, 10)) & 0xFFFF
+    buf[o4 + 10] = (c >> 8).astype(np.uint8)
+    buf[o4 + 11] = (c & 0xFF).astype(np.uint8)
+
+    proto = np.where(v4, buf[off + l3 + 9], buf[off + l3 + 6]).astype(np.int64)
+    l4 = off + np.where(v4, l3 + 20, l3 + 40)
+    l4_len = off + ln - l4
+    cko = l4 + np.where(proto == IPPROTO_UDP, 6, 16)
+    buf[cko] = 0
+    buf[cko + 1] = 0
+    # source + destination address words
+    pseudo = words(off + l3 + 12, 4) if v4.all() else np.where(
+        v4, words(off + l3 + 12, 4), words(off + l3 + 8, 16))
+    pseudo = pseudo + proto + l4_len
+    w = buf[: buf.size // 2 * 2].reshape(-1, 2).astype(np.int64)
+    cs = np.concatenate([[0], np.cumsum((w[:, 0] << 8) | w[:, 1])])
+    end = off + ln
+    s = cs[end // 2] - cs[l4 // 2] + np.where(end % 2 == 1, buf[end - 1].astype(np.int64) << 8, 0)
+    c = ~fold(pseudo + s) & 0xFFFF
+    c = np.where((proto == IPPROTO_UDP) & (c == 0), 0xFFFF, c)
+    buf[cko] = (c >> 8).astype(np.uint8)
+    buf[cko + 1] = (c & 0xFF).astype(np.uint8)
+    return b
+
+
 IMIX_SIZES = np.array([60, 566, 1514])
 IMIX_WEIGHTS = np.array([7, 4, 1])
 
