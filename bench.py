@@ -5,26 +5,34 @@ Metric (BASELINE.json): Mpkts/s classified device-resident.  A "step" is one
 pass of the hot path (one mi_cls_kernel launch through the libodp_cls.so C
 ABI) over one batch of synthetic packets already resident in HBM.
 
-Default workload: BASELINE config 2 -- 1 M x 64 B (60 B buffer) IPv4/UDP per
-GPU, 16 SIP-prefix PMRs (configs[1], the single-GPU config the metric is
-quoted on).  Multi-GPU: one process per GPU (torchrun), each rank classifies
-its own 1 M-packet shard (weak scaling, no data-path collective); the timed
-region is bracketed by barrier + synchronize and the max over ranks is taken.
+Default workload: BASELINE config 3 (configs[2]) -- 1 M IMIX packets
+(60/566/1514 B, 7:4:1, shuffled) per GPU, 256 PMRs over L3+L4 fields, the
+largest configuration that fits one GPU.  The 64 B / 256-rule north-star case
+(config "33") and configs 2, 4 and 5 are reported under `extra`.
+Multi-GPU: one process per GPU (torchrun), each rank classifies its own 1 M
+packet shard (weak scaling, no data-path collective); the timed region is
+bracketed by barrier + synchronize and the max over ranks is taken.
+
+`value` comes from ONE HIP stream: K launches back to back, so the kernel's
+single-launch time (`roofline.kernel_ms`, HIP events on that same stream over
+the same K launches) is never longer than `ms_per_step`.  A two-stream pass
+(consecutive batches alternating over two streams, as a receive path with two
+bursts in flight runs them) is reported as `pipelined` only.
 
 Extra fields on the JSON line:
   roofline      HBM roofline of the dominant kernel: algorithmic bytes
                 (min(len,128) + 6 B descriptor + 16 B result per packet) over
-                the average launch duration, from HIP events on the launch
-                stream in a second, single-stream pass (launches back to back,
-                no overlap, so it agrees with rocprofv3's per-dispatch
-                average); `pipelined_*` are the same bytes over the
-                per-step time of the two-stream `value` pass
-  cpu_baseline  the oracle (scalar C restatement, 1 thread) timed on this
-                host over repeated passes of the same batch
-  e2e           end-to-end rate including pinned H2D of the batch and D2H of
-                the results (recorded, never `value`)
-  extra         config 3 (IMIX, 256 rules) and the 64 B / 256-rule north-star
-                case, timed the same way (rank 0, N=1 only)
+                the average launch duration; `traffic` = HBM bytes per launch
+                from the committed rocprofv3 PMC summary (profiles/)
+  compute       the integer-VALU side for >= 256 rules: reference-equivalent
+                term evaluations per second (the reference's linear scan work
+                on this batch, counted by the oracle) and the kernel's VALU
+                issue fraction from the committed PMC summary
+  cpu_baseline  the oracle (scalar C restatement) timed on this host, 1 thread
+                and one thread per available core (<= 16)
+  parity_vs_oracle  every 16-B record of the timed batch == the oracle's
+  e2e           end-to-end rate including pinned H2D / D2H (never `value`)
+  extra         the other configurations, each timed and parity-checked
 """
 import argparse
 import json
@@ -35,7 +43,11 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+N_SIMD = 256 * 4           # 256 CUs x 4 SIMDs
+SCLK_GHZ = 2.4             # peak engine clock
+WORKLOAD = {2: "config2", 3: "config3", 4: "config4", 5: "config5", 33: "config3_64B",
+            1: "config1", 20: "config2_norules", 34: "config3_64rules"}
 
 
 def parse_args():
@@ -43,14 +55,16 @@ def parse_args():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", type=int, default=2)
+    ap.add_argument("--config", type=int, default=3)
     ap.add_argument("--n", type=int, default=1_000_000, help="packets per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-extra", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--streams", type=int, default=2,
-                    help="HIP streams the consecutive batches alternate over (the timed "
-                         "`value` pass); the roofline pass always uses one stream")
+    ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--timed-only", action="store_true",
+                    help="only the timed single-config pass (profiling runs)")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="HIP streams the timed launches alternate over (1: back to back)")
     ap.add_argument("--rotate", type=int, default=4,
                     help="distinct device copies of the batch, used round-robin, so the "
                          "working set (R x batch) exceeds the 256 MiB Infinity Cache and every "
@@ -102,10 +116,9 @@ def time_device(c, batch, dev, steps, warmup, dist_on=False, rotate=1, streams=1
         b0 = copies[0]
         copies.append(tuple(t.clone() for t in b0[:3]) + (torch.empty_like(b0[3]),))
     stream = torch.cuda.current_stream(dev)
-    # streams > 1: consecutive batches alternate between streams, so one
-    # launch's ramp-up overlaps the previous one's tail (a pipelined receive
-    # path keeps several bursts in flight the same way); copy i always runs on
-    # stream i % streams, so no two in-flight launches share buffers
+    # streams > 1: consecutive batches alternate between streams (copy i
+    # always runs on stream i % streams, so no two in-flight launches share
+    # buffers)
     strm = [stream] + [torch.cuda.Stream(dev) for _ in range(1, max(1, streams))]
     if len(copies) % len(strm):
         raise ValueError("rotate must be a multiple of streams")
@@ -119,8 +132,7 @@ def time_device(c, batch, dev, steps, warmup, dist_on=False, rotate=1, streams=1
     torch.cuda.synchronize(dev)
     # HIP events on the launch stream bracket the timed region (no per-launch
     # events inside it: each record is a host call between launches); the
-    # average launch duration is their span / steps (kernels + the gaps
-    # between back-to-back launches)
+    # average launch duration is their span / steps
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     if dist_on:
@@ -131,7 +143,9 @@ def time_device(c, batch, dev, steps, warmup, dist_on=False, rotate=1, streams=1
     for s_ in strm[1:]:
         s_.wait_event(ev0)
     for i in range(steps):
-        c.classify_device(*arglist[i % len(arglist)])
+        rc = c.classify_device(*arglist[i % len(arglist)])
+        if rc:
+            raise RuntimeError(f"classify failed: {rc}")
     for s_ in strm[1:]:
         stream.wait_stream(s_)
     ev1.record(stream)
@@ -140,7 +154,38 @@ def time_device(c, batch, dev, steps, warmup, dist_on=False, rotate=1, streams=1
         dist.barrier()
     wall = time.perf_counter() - t0
     kms = ev0.elapsed_time(ev1) / steps
+    # the last launch on copy 0 wrote t_out: rerun it so the returned records
+    # belong to copy 0's batch whatever `steps` was
+    c.classify_device(*arglist[0])
+    torch.cuda.synchronize(dev)
     return wall, kms, t_out
+
+
+def records(t_out, n):
+    import numpy as np
+    from odp_amd import rules as R
+    return t_out.cpu().numpy().view(np.uint8).reshape(-1)[: 16 * n].view(R.RESULT_DTYPE)
+
+
+def oracle_parity(prog, batch, got, threads=16):
+    """Bit-exact check of every record against the oracle (multi-threaded)."""
+    import numpy as np
+    from oracle.oracle import Oracle
+    o = Oracle()
+    o.apply(prog)
+    exp = o.classify(batch, threads=threads)
+    return bool(np.array_equal(got, exp))
+
+
+def term_evals_per_pkt(prog, batch, sample=20000):
+    """Reference-equivalent work: terms the reference's linear scan
+    (match_pmr_cos -> verify_pmr) evaluates per packet, on a sample."""
+    from oracle.oracle import Oracle
+    o = Oracle()
+    o.apply(prog)
+    sl = batch.slice(0, min(sample, batch.n))
+    r, t = o.eval_counts(sl)
+    return r / sl.n, t / sl.n
 
 
 def time_e2e(c, batch, dev, steps=5):
@@ -177,53 +222,107 @@ def time_e2e(c, batch, dev, steps=5):
             "note": "pinned H2D of the whole packed batch + descriptors, kernel, D2H results"}
 
 
-def cpu_baseline(prog, batch, seconds, out_gpu):
+def cpu_baseline(prog, batch, seconds):
     """The scalar C restatement (oracle) on this host: first 1 thread, then
     one thread per available core (up to 16, the GPU box's CPU share), each
     thread on a disjoint slice, repeated passes over the batch for about
-    `seconds` / 2 each; also checks the GPU records of the timed batch bit
-    for bit against the single-thread pass."""
-    import numpy as np
+    `seconds` / 2 each."""
     from oracle.oracle import Oracle
     o = Oracle()
     o.apply(prog)
 
-    def timed(threads, budget):
+    def timed(threads, budget, sample):
         t0 = time.perf_counter()
-        res = o.classify(batch, threads=threads)
+        o.classify(sample, threads=threads)
         passes = 1
         while time.perf_counter() - t0 < budget:
-            o.classify(batch, threads=threads)
+            o.classify(sample, threads=threads)
             passes += 1
-        return res, passes, time.perf_counter() - t0
+        return passes, time.perf_counter() - t0
 
-    exp, p1, dt1 = timed(1, seconds / 2)
+    one = batch.slice(0, min(batch.n, 200_000))
+    p1, dt1 = timed(1, seconds / 2, one)
     cores = max(1, min(16, len(os.sched_getaffinity(0))))
-    _, pn, dtn = timed(cores, seconds / 2)
-    parity = bool(np.array_equal(out_gpu, exp))
-    v1 = p1 * batch.n / dt1 / 1e6
+    pn, dtn = timed(cores, seconds / 2, batch)
+    v1 = p1 * one.n / dt1 / 1e6
     vn = pn * batch.n / dtn / 1e6
     return {"value": round(vn, 3), "unit": "Mpkts/s", "cores": cores, "kind": "port",
             "single_core": round(v1, 3),
             "sample": f"{pn} passes over the same {batch.n}-packet batch with {cores} threads "
-                      f"({dtn:.1f} s) and {p1} passes with 1 thread ({dt1:.1f} s); "
-                      f"oracle/odp_cls_oracle.c, gcc -O2, disjoint slices per thread"}, parity
+                      f"({dtn:.1f} s) and {p1} passes over its first {one.n} packets with 1 "
+                      f"thread ({dt1:.1f} s); oracle/odp_cls_oracle.c, gcc -O2, disjoint "
+                      f"slices per thread"}
 
 
-def load_traffic(cfg, n):
+def load_pmc(cfg, n):
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
             d = json.load(f)
-        e = d.get(f"config{cfg}_n{n}")
-        return None if e is None else e["hbm_bytes_per_launch"]
+        return d.get(f"{WORKLOAD[cfg]}_n{n}") or d.get(f"config{cfg}_n{n}")
     except (OSError, ValueError, KeyError):
         return None
 
 
+def compute_roof(prog, batch, kms, pmc):
+    """Integer-VALU side: reference-equivalent term evaluations / s, and the
+    kernel's VALU issue fraction (a wave64 VALU op occupies its SIMD for 4
+    cycles; SQ_INSTS_VALU from the committed PMC summary)."""
+    rules_pp, terms_pp = term_evals_per_pkt(prog, batch)
+    out = {"bound": "valu", "ref_rules_tested_per_pkt": round(rules_pp, 3),
+           "ref_term_evals_per_pkt": round(terms_pp, 3),
+           "term_evals_per_s": round(terms_pp * batch.n / (kms * 1e-3), 1)}
+    v = (pmc or {}).get("SQ_INSTS_VALU_per_launch")
+    if v:
+        issue = v * 4.0 / (kms * 1e-3 * SCLK_GHZ * 1e9 * N_SIMD)
+        out.update({"valu_insts_per_launch": v, "valu_issue_frac": round(issue, 4),
+                    "note": "issue frac = SQ_INSTS_VALU x 4 cycles / (kernel time x "
+                            f"{SCLK_GHZ} GHz x {N_SIMD} SIMDs)"})
+    return out
+
+
+def bench_cfg(cls, cfg, a, dev, local, steps, warmup, pktin_opt=0, parity=True, full_bytes=False):
+    """Time one extra configuration (single stream and two streams), check
+    its records against the oracle."""
+    import numpy as np
+    from odp_amd import pktgen as pg, rules as R
+    b2, p2 = make_workload(cfg, a.n, 0)
+    if pktin_opt:
+        pg.set_checksums(b2)
+    c2 = cls.Classifier(gpu=local)
+    c2.apply(p2)
+    if pktin_opt:
+        c2.set_pktin_opt(pktin_opt)
+    w1, k1, t_out = time_device(c2, b2, dev, steps, warmup, rotate=a.rotate)
+    got = records(t_out, b2.n).copy()
+    w2, _, _ = time_device(c2, b2, dev, steps, warmup, rotate=a.rotate, streams=2)
+    c2.close()
+    nbytes = (int(b2.len.astype(np.int64).sum()) + 22 * b2.n) if full_bytes else b2.header_bytes()
+    e = {"workload": WORKLOAD[cfg], "rules": R.rule_count(p2),
+         "mpkts_per_s": round(b2.n * steps / w1 / 1e6, 2),
+         "mpkts_per_s_2streams": round(b2.n * steps / w2 / 1e6, 2),
+         "kernel_ms": round(k1, 5), "bytes_per_launch": nbytes,
+         "roofline_frac": round(nbytes / (k1 * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)}
+    pmc = load_pmc(cfg, b2.n) if not pktin_opt else None
+    if pmc:
+        e["traffic"] = pmc.get("hbm_bytes_per_launch")
+    if R.rule_count(p2) >= 256 and not pktin_opt:
+        e["compute"] = compute_roof(p2, b2, k1, pmc)
+    if parity:
+        o_prog = p2
+        if pktin_opt:
+            from oracle.oracle import Oracle
+            o = Oracle(pktin_opt=pktin_opt)
+            o.apply(o_prog)
+            e["parity_vs_oracle"] = bool(np.array_equal(got, o.classify(b2, threads=16)))
+            e["checksum_ok"] = bool(np.all((got["err"] & 0x44) == 0))
+        else:
+            e["parity_vs_oracle"] = oracle_parity(o_prog, b2, got)
+    return e
+
+
 def main():
     a = parse_args()
-    import numpy as np
     import torch
     import torch.distributed as dist
 
@@ -241,12 +340,8 @@ def main():
     c = cls.Classifier(gpu=local)
     c.apply(prog)
 
-    wall, kms_pipe, t_out = time_device(c, batch, dev, a.steps, a.warmup, dist_on, a.rotate,
-                                        a.streams)
-    if a.streams > 1:
-        _, kms, _ = time_device(c, batch, dev, a.steps, a.warmup, dist_on, a.rotate, 1)
-    else:
-        kms = kms_pipe
+    wall, kms, t_out = time_device(c, batch, dev, a.steps, a.warmup, dist_on, a.rotate,
+                                   a.streams)
     if dist_on:
         t = torch.tensor([wall], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -255,10 +350,10 @@ def main():
     value = total_pkts / wall / 1e6
     bytes_launch = batch.header_bytes()
     achieved = bytes_launch / (kms * 1e-3) / 1e9
-    achieved_pipe = bytes_launch / (kms_pipe * 1e-3) / 1e9
     res = None
     if rank == 0:
-        out = t_out.cpu().numpy().view(np.uint8).reshape(-1)[: 16 * batch.n].view(R.RESULT_DTYPE)
+        out = records(t_out, batch.n).copy()
+        pmc = load_pmc(a.config, batch.n)
         line = {
             "metric": "Mpkts/s classified device-resident",
             "value": round(value, 2),
@@ -266,73 +361,53 @@ def main():
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
-            "ms_per_step": round(wall / a.steps * 1e3, 4),
+            "ms_per_step": round(wall / a.steps * 1e3, 5),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic",
-            "config": {"workload": f"config{a.config}", "packets_per_gpu": batch.n,
+            "config": {"workload": WORKLOAD[a.config], "packets_per_gpu": batch.n,
                        "rules": R.rule_count(prog), "cos": R.cos_count(prog),
-                       "frame_bytes": "60 (64 B on the wire)" if a.config == 2 else "mixed",
+                       "frame_bytes": "60 (64 B on the wire)" if a.config in (2, 33)
+                       else "IMIX 60/566/1514 7:4:1" if a.config == 3 else "mixed",
+                       "streams": a.streams, "rotate": a.rotate,
                        "parallelism": f"shard{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "traffic": load_traffic(a.config, batch.n),
+                         "traffic": (pmc or {}).get("hbm_bytes_per_launch"),
                          "kernel": "mi_cls_kernel", "kernel_ms": round(kms, 5),
                          "bytes_per_launch": bytes_launch,
-                         "pipelined_achieved": round(achieved_pipe, 2),
-                         "pipelined_frac": round(achieved_pipe / HBM_PEAK_GBS, 5),
-                         "streams": a.streams},
+                         "traffic_source": (pmc or {}).get("source")},
         }
-        if world == 1:
+        if world == 1 and not a.timed_only:
+            if R.rule_count(prog) >= 256:
+                line["compute"] = compute_roof(prog, batch, kms, pmc)
+            if not a.no_parity:
+                line["parity_vs_oracle"] = oracle_parity(prog, batch, out)
+            w2, _, _ = time_device(c, batch, dev, a.steps, a.warmup, rotate=a.rotate, streams=2)
+            line["pipelined"] = {"streams": 2, "mpkts_per_s": round(batch.n * a.steps / w2 / 1e6, 2),
+                                 "ms_per_step": round(w2 / a.steps * 1e3, 5)}
             try:
                 line["e2e"] = time_e2e(c, batch, dev)
             except Exception as e:   # recorded, never fatal
                 line["e2e"] = {"error": str(e)}
             if not a.no_cpu:
-                cb, parity = cpu_baseline(prog, batch, a.cpu_seconds, out)
-                line["cpu_baseline"] = cb
-                line["parity_vs_oracle"] = parity
+                line["cpu_baseline"] = cpu_baseline(prog, batch, a.cpu_seconds)
             if not a.no_extra:
                 extra = {}
-                names = {33: "config3_64B_256rules", 3: "config3_imix_256rules",
-                         4: "config4_imix_v4v6_1024rules", 5: "config5_vlan_tree_4096rules"}
-                for cfg in (33, 3, 4, 5):
-                    b2, p2 = make_workload(cfg, a.n, 0)
-                    c2 = cls.Classifier(gpu=local)
-                    c2.apply(p2)
-                    k_steps = max(5, a.steps // 5)
-                    w2, _, _ = time_device(c2, b2, dev, k_steps, 3, rotate=a.rotate,
-                                           streams=a.streams)
-                    _, k2, _ = time_device(c2, b2, dev, k_steps, 3, rotate=a.rotate)
-                    c2.close()
-                    ach = b2.header_bytes() / (k2 * 1e-3) / 1e9
-                    extra[names[cfg]] = {
-                        "mpkts_per_s": round(b2.n * k_steps / w2 / 1e6, 2),
-                        "kernel_ms": round(k2, 4), "roofline_frac": round(ach / HBM_PEAK_GBS, 5),
-                        "rules": R.rule_count(p2)}
+                k_steps = max(5, a.steps // 2)
+                for cfg in (33, 2, 4, 5):
+                    if cfg == a.config:
+                        continue
+                    extra[WORKLOAD[cfg]] = bench_cfg(cls, cfg, a, dev, local, k_steps, 3,
+                                                     parity=not a.no_parity)
                 # pktin checksum validation (IPv4 header, UDP/TCP sums over the
                 # whole frame): config 3 IMIX with valid checksums; the kernel
                 # reads every frame byte, so the bytes are frame + 22 B
-                from odp_amd import pktgen as pg
-                b2, p2 = make_workload(3, a.n, 0)
-                pg.set_checksums(b2)
-                c2 = cls.Classifier(gpu=local)
-                c2.apply(p2)
-                c2.set_pktin_opt(0x3C)
-                k_steps = max(5, a.steps // 5)
-                w2, _, _ = time_device(c2, b2, dev, k_steps, 3, rotate=a.rotate,
-                                       streams=a.streams)
-                _, k2, _ = time_device(c2, b2, dev, k_steps, 3, rotate=a.rotate)
-                c2.close()
-                fb = int(b2.len.astype(np.int64).sum()) + 22 * b2.n
-                extra["config3_imix_256rules_checksums"] = {
-                    "mpkts_per_s": round(b2.n * k_steps / w2 / 1e6, 2),
-                    "kernel_ms": round(k2, 4),
-                    "roofline_frac": round(fb / (k2 * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
-                    "bytes_per_launch": fb, "pktin_opt": "ipv4/udp/tcp/sctp checksums",
-                    "rules": R.rule_count(p2)}
+                extra["config3_checksums"] = bench_cfg(cls, 3, a, dev, local, k_steps, 3,
+                                                       pktin_opt=0x3C, parity=not a.no_parity,
+                                                       full_bytes=True)
                 line["extra"] = extra
         res = line
         print(json.dumps(res), flush=True)

@@ -780,17 +780,33 @@ static int bytes_match(const pkt_t *k, uint32_t o, const orc_term_t *t)
 	return 1;
 }
 
+/* Work counters of the reference's linear scan on this thread: PMRs
+ * verify_pmr was called on, and terms it evaluated (its loop stops at the
+ * first failing term, :1386-1512).  Read by orc_eval_counts() for bench.py's
+ * compute roof ("reference-equivalent term evaluations"). */
+static __thread uint64_t n_rules_tested, n_terms_tested;
+
+void orc_eval_counts(uint64_t *rules, uint64_t *terms)
+{
+	*rules = n_rules_tested;
+	*terms = n_terms_tested;
+	n_rules_tested = n_terms_tested = 0;
+}
+
 /* verify_pmr (:1363-1515) with the verify_pmr_<term> helpers (:931-1357) */
 static int verify_pmr(const orc_pmr_t *r, const pkt_t *k, const orc_parser_t *prs)
 {
 	uint64_t f = prs->input_flags;
 	int i;
 
+	n_rules_tested++;
 	if (!r->valid)
 		return 0;
 	for (i = 0; i < r->num_terms; i++) {
 		const orc_term_t *t = &r->t[i];
 		int ok;
+
+		n_terms_tested++;
 
 		switch (t->term) {
 		case T_LEN: {

@@ -66,6 +66,8 @@ def lib():
         L.orc_softrss.restype = u32
         L.orc_pktin_opt_set.argtypes = [C.c_uint64]
         L.orc_pktin_opt_set.restype = None
+        L.orc_eval_counts.argtypes = [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        L.orc_eval_counts.restype = None
         _lib = L
     return _lib
 
@@ -132,6 +134,15 @@ class Oracle:
             self.L.orc_classify_batch_mt(buf.ctypes.data, off.ctypes.data, ln.ctypes.data, n,
                                          out.ctypes.data, self.max_hops, threads)
         return out[:n]
+
+    def eval_counts(self, batch):
+        """Classify ``batch`` on this thread and return the reference's
+        linear-scan work for it: (PMRs verified, terms evaluated)."""
+        r, t = C.c_uint64(), C.c_uint64()
+        self.L.orc_eval_counts(C.byref(r), C.byref(t))   # reset
+        self.classify(batch)
+        self.L.orc_eval_counts(C.byref(r), C.byref(t))
+        return r.value, t.value
 
     def stats_packets(self, cos_handle):
         return self.L.orc_cos_stats_packets(cos_handle)

@@ -128,11 +128,13 @@ def term_cases():
               [(create_packet(vlan=True, tci0=0x123), MATCH),
                (create_packet(vlan=True, qinq=True, tci1=0x123), MATCH),
                (create_packet(), NO_MATCH)]))
-    # test_pmr_term_ipv4_addr :1351-1405 (10.0.0.77 SIP, 10.0.0.99 DIP /32 style)
+    # test_pmr_term_ipv4_addr :1351-1395: rule 10.0.0.88/32 (SIP) or
+    # 10.0.0.99/32 (DIP); the MATCH packet carries both addresses (src
+    # 10.0.0.88, dst 10.0.0.99, :1380-1382), the NO_MATCH packet the defaults
     for dst in (False, True):
         term = R.PMR_DIP_ADDR if dst else R.PMR_SIP_ADDR
-        a = "10.0.0.99" if dst else "10.0.0.77"
-        pk = create_packet(**({"dst": a} if dst else {"src": a}))
+        a = "10.0.0.99" if dst else "10.0.0.88"
+        pk = create_packet(src="10.0.0.88", dst="10.0.0.99")
         C.append((f"ipv4_{'d' if dst else 's'}addr", single(R.t_ip4(term, a, 32)),
                   [(pk, MATCH), (create_packet(), NO_MATCH)]))
     # cls_pmr_term_ipv6daddr / saddr :1407-1476 (mask: last 6 bytes)

@@ -223,6 +223,21 @@ def test_config3_full_size_properties(built, gpu):
     assert np.array_equal(got, gpu_run(prog, b))
 
 
+@pytest.mark.parametrize("cfg,kw", [(3, {}), (3, {"size": 60}), (4, {}), (5, {}), (2, {})],
+                         ids=["config3_imix", "config3_64B", "config4", "config5", "config2"])
+def test_configs_full_size(built, gpu, cfg, kw):
+    """BASELINE configs at full size (1 M packets: one GPU's shard for
+    configs 4 and 5): every record bit-exact vs the multithreaded oracle."""
+    from oracle.oracle import Oracle
+    b, prog = (R.config3(1_000_000, **kw) if cfg == 3 else R.CONFIGS[cfg](1_000_000))
+    got = gpu_run(prog, b)
+    o = Oracle()
+    o.apply(prog)
+    exp = o.classify(b, threads=16)
+    assert_same(got, exp, b, f"config {cfg} {kw} full size")
+    assert summary(got)["enq"] > 0
+
+
 @pytest.mark.parametrize("case", RC.term_cases() + RC.chain_cases(), ids=lambda c: c[0])
 def test_reference_known_answers_gpu(built, gpu, case):
     """The reference validation suite's MATCH / NO_MATCH expectations on the

@@ -45,8 +45,9 @@ def _run_case(tmp_path, prog, frames, mode="sched", pktio="pcap", cos_pools=1, l
 def test_example_classifier_udp64(built, gpu):
     """The reference's own acceptance run: 100 packets to queue1, 100 to
     DefaultCos, exit status 0."""
-    if not os.path.exists(H.EXAMPLE):
-        pytest.skip("example binary not built")
+    # the binary is built in the build container and travels with the tree:
+    # missing on the GPU box is a failure, not a skip
+    assert os.path.exists(H.EXAMPLE), f"{H.EXAMPLE} missing: run __graft_entry__.build()"
     r = subprocess.run([H.EXAMPLE, "-t", "1", "-i", f"pcap:in={UDP64}", "-m", "0", "-p",
                         "ODP_PMR_SIP_ADDR:10.10.10.0:0xFFFFFF00:queue1", "-P", "-C",
                         "queue1:100", "-C", "DefaultCos:100"],
@@ -64,8 +65,9 @@ def test_example_classifier_udp64(built, gpu):
 
 def test_example_classifier_two_workers_dmac(built, gpu):
     """Two worker threads, a DMAC rule, no dedicated CoS pools (-d 0)."""
-    if not os.path.exists(H.EXAMPLE):
-        pytest.skip("example binary not built")
+    # the binary is built in the build container and travels with the tree:
+    # missing on the GPU box is a failure, not a skip
+    assert os.path.exists(H.EXAMPLE), f"{H.EXAMPLE} missing: run __graft_entry__.build()"
     r = subprocess.run([H.EXAMPLE, "-t", "1", "-c", "2", "-d", "0", "-i", f"pcap:in={UDP64}",
                         "-m", "0", "-p", "ODP_PMR_DMAC:02-00-00-00-00-02:ffffffffffff:mac",
                         "-P", "-C", "mac:200"],
