@@ -219,6 +219,14 @@ int mi_cls_stats_enable(mi_cls_ctx_t *ctx, const uint32_t stats_mask[8]);
 int mi_cls_stats_read(mi_cls_ctx_t *ctx, uint64_t *host_counters, uint32_t num);
 int mi_cls_stats_reset(mi_cls_ctx_t *ctx);
 
+/* Host-only (no device needed): assemble a compiled table into the private
+ * device encoding and describe it.  info[0] total 32-bit words, [1] words of
+ * the per-lane "hot" region (copied to LDS when it fits), [2] CoS with a
+ * classification block, [3..6] blocks per engine (direct, candidate,
+ * bitmap, wide bitmap), [7] 1 if some rule leads to a CoS with rules.
+ * n >= 8.  Used by tests and tools to check engine selection on the CPU. */
+int mi_cls_program_info(const void *tbl, size_t bytes, uint32_t *info, uint32_t n);
+
 /* Last error string for the context (static storage, never NULL). */
 const char *mi_cls_strerror(int err);
 

@@ -142,6 +142,7 @@ def _load():
         "mi_cls_rules_load": (i32, [vp, vp, C.c_size_t, vp]),
         "mi_cls_classify": (i32, [vp, vp, vp, vp, u32, vp, vp]),
         "mi_cls_strerror": (C.c_char_p, [i32]),
+        "mi_cls_program_info": (i32, [vp, C.c_size_t, C.POINTER(u32), u32]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -262,6 +263,17 @@ class Classifier:
         buf = C.create_string_buffer(n)
         assert self.L.odp_amd_cls_compile(self.pktio, buf, n) == n
         return buf.raw
+
+    def program_info(self) -> dict:
+        """Device encoding of the current rule snapshot (host only)."""
+        blob = self.compile()
+        info = (C.c_uint32 * 8)()
+        rc = self.L.mi_cls_program_info(blob, len(blob), info, 8)
+        if rc:
+            raise RuntimeError(f"mi_cls_program_info: {rc}")
+        return {"words": info[0], "hot_words": info[1], "blocks": info[2],
+                "direct": info[3], "candidate": info[4], "bitmap": info[5], "wide": info[6],
+                "tree": bool(info[7])}
 
     # -- data path -------------------------------------------------------
     def classify_device(self, d_buf, d_off, d_len, n, d_out, stream=0):

@@ -117,23 +117,34 @@ struct Pkt {
 	const uint32_t *w;      // &W[lane]
 	const uint8_t *g;       // packet start in HBM
 	uint32_t len;           // frame_len
+	uint32_t win;           // bytes of the frame staged in LDS this tile (64 or WIN;
+	                        // wave-uniform): bytes [0, min(len, win)) are in
+	                        // the window, bytes past the frame read 0
 };
 
+// One byte; past the staged window it comes from HBM (the general parser and
+// the rare far field), past the frame it is 0.
 __device__ __forceinline__ uint32_t rb(const Pkt &k, uint32_t o)
 {
-	if (o < WIN)
+	if (o < k.win)
 		return (k.w[(o >> 2) * RS] >> ((o & 3u) * 8u)) & 0xffu;
 	return o < k.len ? (uint32_t)k.g[o] : 0u;
 }
 
-// 4 bytes starting at byte offset o, little-endian (== the reference's raw load)
+// 4 bytes starting at byte offset o, little-endian (== the reference's raw
+// load).  The LDS read is unconditional (row index clamped into the window
+// and its zero rows), so lanes do not diverge; a wave-uniform branch fixes up
+// the lanes whose 4 bytes reach past the staged window (bytes from HBM).
 __device__ __forceinline__ uint32_t r32(const Pkt &k, uint32_t o)
 {
-	if (o <= WIN - 4u) {
-		uint32_t i = o >> 2;
-		return __builtin_amdgcn_alignbyte(k.w[(i + 1) * RS], k.w[i * RS], o & 3u);
+	const uint32_t i = min(o >> 2, (uint32_t)(WIN / 4 + 1));
+	uint32_t v = __builtin_amdgcn_alignbyte(k.w[(i + 1) * RS], k.w[i * RS], o & 3u);
+	const bool far = o + 4u > k.win;
+	if (__ballot(far) != 0ull) {
+		if (far)
+			v = rb(k, o) | (rb(k, o + 1) << 8) | (rb(k, o + 2) << 16) | (rb(k, o + 3) << 24);
 	}
-	return rb(k, o) | (rb(k, o + 1) << 8) | (rb(k, o + 2) << 16) | (rb(k, o + 3) << 24);
+	return v;
 }
 
 __device__ __forceinline__ uint32_t r16(const Pkt &k, uint32_t o)
@@ -653,7 +664,12 @@ __device__ __forceinline__ Parsed parse_fast(const Pkt &k, const uint32_t *l4tab
 			lb[i] = __builtin_amdgcn_alignbyte(m[i + 1], m[i], 2u);
 		const bool tcp = chk && kc == L4K_TCP, udp = chk && kc == L4K_UDP;
 		const bool sctp = chk && kc == L4K_SCTP;
-		sl = sl || (chk && l4 + 18u > WIN);   // past the window
+		// bytes the checks below use: TCP data offset (l4+12), UDP ports and
+		// length (l4..l4+5) and, for destination port 4500, the NAT-T marker
+		// (l4+8..l4+11); a lane whose bytes are not all staged takes the
+		// general parser (the unused bytes of m[] may lie past the window)
+		const uint32_t l4need = tcp ? 13u : (udp ? (((lb[0] >> 16) == 0x9411u) ? 12u : 6u) : 0u);
+		sl = sl || (chk && l4 + l4need > k.win);
 		// TCP (parse_tcp, :299-316)
 		const bool tcp_drop = tcp && l4 + 20u > len;
 		err |= (tcp && !tcp_drop && ((lb[3] & 0xffu) >> 4) < 5u) ? E_TCP : 0u;
@@ -701,6 +717,9 @@ struct Fields {
 // "l2 && l3 valid" (custom L3) is F_L2 plus the l3 != invalid test in
 // field_off.
 enum { FB_FRAME = 0, FB_L3 = 1, FB_L4 = 2 };
+// classification-block pseudo kind: UDP and TCP port terms with one mask
+// (class_of), the raw port word at l4 tagged with the protocol
+#define K_L4PORT 0x40u
 struct FDesc {
 	uint32_t base, add, alt, altf, gate;
 };
@@ -719,6 +738,7 @@ __host__ __device__ inline FDesc fdesc(uint32_t kind, uint32_t toff)
 	case MI_K_UDP_SPORT: d = { FB_L4, 0u, 0u, 0u, F_UDP }; break;
 	case MI_K_TCP_DPORT:
 	case MI_K_TCP_SPORT: d = { FB_L4, 0u, 0u, 0u, F_TCP }; break;
+	case K_L4PORT: d = { FB_L4, 0u, 0u, 0u, F_UDP | F_TCP }; break;
 	case MI_K_SIP: d = { FB_L3, 12u, 12u, 0u, F_IPV4 }; break;
 	case MI_K_DIP: d = { FB_L3, 16u, 16u, 0u, F_IPV4 }; break;
 	case MI_K_SIP6: d = { FB_L3, 8u, 8u, 0u, F_IPV6 }; break;
@@ -861,7 +881,10 @@ typedef const __attribute__((address_space(3))) uint32_t *lword_t;   // LDS
 typedef const __attribute__((address_space(1))) uint32_t *gword_t;   // HBM
 
 enum { DH_MAGIC = 0, DH_NCOS, DH_DEFAULT, DH_ERROR, DH_DEFAULT_VALID, DH_USED, DH_MAX_HOPS,
-       DH_HOT_OFF, DH_PROG_OFF, DH_TOTAL, DH_HOT_WORDS, DH_WORDS = 16 };
+       DH_HOT_OFF, DH_PROG_OFF, DH_TOTAL, DH_HOT_WORDS,
+       // furthest byte past L3 / L4 / the frame start any term (or the hash
+       // queue tuple) of the program reads: the kernel's window predictor
+       DH_L3END, DH_L4END, DH_FREND, DH_WORDS = 16 };
 #define DEV_MAGIC 0x33564544u   // "DEV3"
 #define REC_WORDS 16u
 #define COS_WORDS 4u
@@ -881,6 +904,7 @@ enum { DH_MAGIC = 0, DH_NCOS, DH_DEFAULT, DH_ERROR, DH_DEFAULT_VALID, DH_USED, D
 #define BVF_SPECIAL 1u          // LEN / PCP / DSCP: special_value()
 #define BVF_CUSTOM 2u           // custom frame / L3: length test
 #define BVF_L3 4u               // custom L3: l3 must be valid
+#define BVF_TAG 8u              // merged UDP/TCP port class: protocol tag at bit cr(3)
 #define BV_EMPTY 0xFFFFFFFFu
 #define BV_NONE 0xFFFFFFFEu
 
@@ -948,6 +972,16 @@ __device__ __forceinline__ uint32_t bv_fold(const uint32_t k[4])
 	return h ^ (h >> 15);
 }
 
+// Cuckoo bucket of a key: x = the key word (one-word keys) or bv_fold (longer
+// keys), folded to 24 bits that depend on every key bit, times a 24-bit
+// multiplier (v_mul_u32_u24, full rate), top `kb` bits of the low 32 bits of
+// the product: 2^kb buckets.  host_bucket() is the same arithmetic.
+__device__ __forceinline__ uint32_t bv_bucket(uint32_t x, uint32_t m, uint32_t kb)
+{
+	// (__umul24 returns int: shift the unsigned product)
+	return (uint32_t)__umul24(x ^ (x >> 16), m) >> (32u - kb);
+}
+
 // Word readers of a classification block: wave-uniform blocks are read with
 // scalar loads from HBM (DescU), per-lane blocks from the hot region (LDS or
 // HBM, DescL).
@@ -987,6 +1021,8 @@ __device__ __forceinline__ bool bv_key(const D &cr, const Pkt &k, const Parsed &
 		present = present && ((dfl & BVF_L3) == 0u || x.l3 != 0xFFFFu) &&
 			  !(x.k.len <= o + cr(4));
 	key[0] = r32(k, o) & cr(5);
+	if (dfl & BVF_TAG)   // merged UDP/TCP port class
+		key[0] |= ((x.f & F_UDP) ? 1u : 2u) << cr(3);
 	if (nk > 1u) {
 		key[1] = r32(k, o + 4u) & cr(6);
 		if (nk > 2u) {
@@ -997,32 +1033,42 @@ __device__ __forceinline__ bool bv_key(const D &cr, const Pkt &k, const Parsed &
 	return present;
 }
 
-// Two-choice cuckoo lookup: the key sits in slot s1 or s2 (both read at
-// once, no probe loop).  A slot is nk key words and a value word; an empty
-// slot has key words 0 and value 0, so "key equal and value non-zero" is a
-// hit.  Returns the hit slot's value, or 0 on a miss.
+// 16-byte read of the hot region (LDS: ds_read_b128, HBM: global dwordx4);
+// i is a multiple of 4 (hot-region blocks, buckets and rows are 16-B aligned)
+__device__ __forceinline__ u32x4 ld4(lword_t H, uint32_t i)
+{
+	return *(const __attribute__((address_space(3))) u32x4 *)(H + i);
+}
+__device__ __forceinline__ u32x4 ld4(gword_t H, uint32_t i)
+{
+	return *(const __attribute__((address_space(1))) u32x4 *)(H + i);
+}
+
+// Two-choice cuckoo lookup (both candidate buckets read at once, no probe
+// loop).  One-word keys: buckets of two (key, value) slots, 16 B, read with
+// one 16-B load each.  Longer keys: one slot of nk key words + value per
+// bucket.  An empty slot has key words 0 and value 0, and a key sits in at
+// most one slot, so OR-ing the values of the slots whose key words equal the
+// packet's gives the hit's value, or 0 on a miss.
 template <typename D, typename T>
 __device__ __forceinline__ uint32_t bv_lookup(const D &cr, T H, const uint32_t key[4], bool act)
 {
+	// ns = log2 of the bucket count
 	const uint32_t nk = cr(1), ns = cr(9), tbl = cr(10), m1 = cr(11), m2 = cr(12);
 	uint32_t val = 0;
 	if (nk == 1u) {
-		// one-word keys (the common case): bv_fold with zero upper words,
-		// two-word slots
-		uint32_t f = key[0] * 0x9E3779B1u;
-		f ^= f >> 15;
-		const uint32_t a1 = tbl + 2u * __umulhi(f * m1, ns);
-		const uint32_t a2 = tbl + 2u * __umulhi(f * m2, ns);
-		const uint32_t k1 = H[a1], v1 = H[a1 + 1u], k2 = H[a2], v2 = H[a2 + 1u];
-		val = (k2 == key[0]) ? v2 : 0u;
-		val = (k1 == key[0] && v1 != 0u) ? v1 : val;
+		// one-word keys (the common case): bv_fold with zero upper words
+		const u32x4 b1 = ld4(H, tbl + 4u * bv_bucket(key[0], m1, ns));
+		const u32x4 b2 = ld4(H, tbl + 4u * bv_bucket(key[0], m2, ns));
+		val = (b1[0] == key[0] ? b1[1] : 0u) | (b1[2] == key[0] ? b1[3] : 0u) |
+		      (b2[0] == key[0] ? b2[1] : 0u) | (b2[2] == key[0] ? b2[3] : 0u);
 		return act ? val : 0u;
 	}
 	const uint32_t f = bv_fold(key);
 	const uint32_t sw = nk + 1u;
 #pragma unroll
 	for (uint32_t s = 0; s < 2; ++s) {
-		const uint32_t a = tbl + __umulhi(f * (s ? m2 : m1), ns) * sw;
+		const uint32_t a = tbl + bv_bucket(f, s ? m2 : m1, ns) * sw;
 		bool e = H[a] == key[0] && H[a + 1] == key[1];
 		if (nk > 2)
 			e = e && H[a + 2] == key[2] && H[a + 3] == key[3];
@@ -1071,7 +1117,10 @@ __device__ __forceinline__ void bv_eval(const D &blk, T H, bool act, const Pkt &
 		// region, BV_WIDE_WORDS words each, zero past the rule count; a miss
 		// takes the class's miss row) and the alive row; the lowest set bit
 		// is the first holding rule
-		const uint32_t ar = blk(4);
+		// rows are split in halves: words 0-3 at the value, words 4-7
+		// `half` words further (consecutive rows are then 16 B apart, so the
+		// 16-lane groups of a 16-B LDS read spread over all 64 banks)
+		const uint32_t ar = blk(4), half = blk(7);
 		uint32_t acc[BV_WIDE_WORDS];
 #pragma unroll
 		for (uint32_t i = 0; i < BV_WIDE_WORDS; ++i)
@@ -1084,9 +1133,12 @@ __device__ __forceinline__ void bv_eval(const D &blk, T H, bool act, const Pkt &
 				const bool present = bv_key(cr, k, p, x, key);
 				const uint32_t val = bv_lookup(cr, H, key, act && present);
 				const uint32_t ro = val != 0u ? val : cr(2);
+				const u32x4 r0 = ld4(H, ro), r1 = ld4(H, ro + half);
 #pragma unroll
-				for (uint32_t i = 0; i < BV_WIDE_WORDS; ++i)
-					acc[i] &= H[ro + i];
+				for (uint32_t i = 0; i < 4; ++i) {
+					acc[i] &= r0[i];
+					acc[4 + i] &= r1[i];
+				}
 			}
 		}
 #pragma unroll
@@ -1219,6 +1271,12 @@ struct KArgs {
 	unsigned long long *diag;    // DIAG_STAMPS builds only
 	uint32_t stats_mask[8];
 	uint32_t opt;                // pktin options (OPT_*), 0: none
+	// window hint across launches of a context: a wave of block 0 whose
+	// frames needed bytes 64.. stores this launch's sequence number `seq` in
+	// *hint; the next launch (seq + 1) starts its predictor from it.  Only a
+	// performance hint -- results never depend on it.
+	uint32_t *hint;
+	uint32_t seq;
 };
 
 __device__ __forceinline__ bool stats_bit(const KArgs &a, uint32_t c)
@@ -1242,7 +1300,7 @@ static_assert(NPIECE == 8 || NPIECE == 6, "WIN must be 96 or 128");
 // when some frame of the tile is longer than 64 B (returns true).  Pieces
 // wholly past a frame get an out-of-range offset and read as zero.
 __device__ __forceinline__ bool load_window(__amdgpu_buffer_rsrc_t rs, uint32_t off, uint32_t len,
-					    uint32_t lane, u32x4 d[NPIECE])
+					    uint32_t lane, u32x4 d[NPIECE], bool want_hi, uint32_t &win)
 {
 	const uint32_t q = lane & 3u, pp = lane >> 2;
 #pragma unroll
@@ -1253,7 +1311,12 @@ __device__ __forceinline__ bool load_window(__amdgpu_buffer_rsrc_t rs, uint32_t 
 		const uint32_t vo = 16u * q < L ? o + 16u * q : OOB_OFF;
 		d[r] = __builtin_amdgcn_raw_buffer_load_b128(rs, vo, 0, LOAD_AUX);
 	}
-	const bool hi = __ballot(len > 64u) != 0ull;
+	// phase B only when some frame is longer than 64 B and the window
+	// predictor wants bytes 64.. (want_hi); otherwise a tile with long frames
+	// stages 64 B per frame and reads the rare bytes past them from HBM
+	const bool any_long = __ballot(len > 64u) != 0ull;
+	const bool hi = any_long && want_hi;
+	win = (any_long && !hi) ? 64u : (uint32_t)WIN;
 	if (hi) {
 		const uint32_t qb = lane % NB, pb = lane / NB;
 #pragma unroll
@@ -1345,7 +1408,7 @@ __device__ __forceinline__ void wave_lds_sync()
 // phase issues no vector memory loads, so nothing it waits for sits behind
 // the next tile's prefetch in the (in-order) vmcnt queue.  !LT reads the hot
 // region from HBM (large rule sets).
-extern __shared__ uint32_t s_dyn[];
+extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
 
 // NW = waves per block: 4 (each block copies the hot region for itself), or
 // 16 = one block per CU whose 16 waves share one LDS copy of a larger hot
@@ -1360,6 +1423,10 @@ __global__ __launch_bounds__(NW * WAVE, MIN_WAVES_PER_EU) void mi_cls_kernel(KAr
 	const uint32_t lane = threadIdx.x & (WAVE - 1);
 	const uint32_t wave = threadIdx.x >> 6;
 	uint32_t *W = s_win + wave * RS * WROWS;
+#ifdef DIAG_STAMPS
+	unsigned long long st_acc[NSTAMP] = { 0 }, st_last;
+	asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_last) :: "memory");
+#endif
 
 	const cword_t dev = (cword_t)a.dev;
 	const int32_t def_cos = (int32_t)dev[DH_DEFAULT];
@@ -1392,24 +1459,6 @@ __global__ __launch_bounds__(NW * WAVE, MIN_WAVES_PER_EU) void mi_cls_kernel(KAr
 			n_len = a.len[p1];
 		}
 	}
-	if constexpr (LT) {
-		const uint32_t hw = dev[DH_HOT_WORDS];
-		const gword_t src = (gword_t)(a.dev + hot_off);
-		for (uint32_t i = threadIdx.x; i < hw; i += NW * WAVE)
-			s_dyn[i] = src[i];
-		H = (lword_t)s_dyn;
-	} else {
-		H = (gword_t)(a.dev + hot_off);
-	}
-
-	if (stats_on) {
-		for (uint32_t i = threadIdx.x; i < MAX_STATS_COS; i += NW * WAVE)
-			s_cnt[i] = 0;
-	}
-	for (uint32_t i = threadIdx.x; i < 256u; i += NW * WAVE)
-		s_l4[i] = c_l4tab.v[i];
-	__syncthreads();
-
 	// Software pipeline over this wave's tiles (64 packets each): while tile
 	// t is parsed and classified, tile t+1's header windows are in flight
 	// into registers (load_window) and tile t+2's descriptors are being
@@ -1421,25 +1470,60 @@ __global__ __launch_bounds__(NW * WAVE, MIN_WAVES_PER_EU) void mi_cls_kernel(KAr
 		(void *)a.pkts, (short)0, (int)OOB_OFF, 0x00020000);
 	u32x4 d[NPIECE];
 	bool d_hi, hi_rows = true;
+	// window predictor: stage bytes 64..WIN-1 of long frames only while the
+	// frames of the last parsed tile needed them (the fields of its rule
+	// program and its parse reach past byte 64); the first tiles stage them
+#if defined(DIAG_FORCE_LO)
+	bool want_hi = false;     // diagnostic: 64-B windows from the first tile
+#elif defined(DIAG_FORCE_HI)
+	bool want_hi = true;
+#else
+	bool want_hi = a.hint == nullptr || *(const uint32_t *)a.hint + 1u == a.seq;
+#endif
+	bool saw_hi = false;
+	uint32_t d_win = WIN, my_win = WIN;
+	const uint32_t p_l3end = dev[DH_L3END], p_l4end = dev[DH_L4END], p_frend = dev[DH_FREND];
+	// the first tile's windows are in flight during the block setup below
+	if (tile < nt)
+		d_hi = load_window(rs, d_off, d_len, lane, d, want_hi, d_win);
+	if constexpr (LT) {
+		// hot region -> LDS in 16-B pieces (the device program and the
+		// dynamic LDS size are padded to 16 B)
+		const uint32_t hq = (dev[DH_HOT_WORDS] + 3u) >> 2;
+		typedef const __attribute__((address_space(1))) u32x4 *gvec_t;
+		const gvec_t src = (gvec_t)(a.dev + hot_off);
+		u32x4 *dst = (u32x4 *)s_dyn;
+		for (uint32_t i = threadIdx.x; i < hq; i += NW * WAVE)
+			dst[i] = src[i];
+		H = (lword_t)s_dyn;
+	} else {
+		H = (gword_t)(a.dev + hot_off);
+	}
+
+	if (stats_on) {
+		for (uint32_t i = threadIdx.x; i < MAX_STATS_COS; i += NW * WAVE)
+			s_cnt[i] = 0;
+	}
+	for (uint32_t i = threadIdx.x; i < 256u; i += NW * WAVE)
+		s_l4[i] = c_l4tab.v[i];
 	for (uint32_t r = WIN / 4; r < WROWS; ++r)
 		W[r * RS + lane] = 0u;   // pad / zero rows: always zero
+	__syncthreads();
+	STAMP(5);   // block setup (hot-region copy) done
+
 	uint4 prev_rec = make_uint4(0, 0, 0, 0);
 	uint32_t prev_pi = 0;
 	bool prev_valid = false;
-	d_hi = load_window(rs, d_off, d_len, lane, d);
-#ifdef DIAG_STAMPS
-	unsigned long long st_acc[NSTAMP] = { 0 }, st_last;
-	asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_last) :: "memory");
-#endif
 	for (; tile < nt; tile += tstride) {
 		const uint32_t pi = tile * WAVE + lane;
 		const bool valid = pi < a.n;
 		if (!PREFETCH && tile != blockIdx.x * NW + wave) {
 			d_off = valid ? a.off[pi] : 0u;
 			d_len = valid ? (uint32_t)a.len[pi] : 0u;
-			d_hi = load_window(rs, d_off, d_len, lane, d);
+			d_hi = load_window(rs, d_off, d_len, lane, d, want_hi, d_win);
 		}
 		const uint32_t my_off = d_off, my_len = d_len;
+		my_win = d_win;
 
 		wave_lds_sync();   // previous tile's window reads are done
 		store_window(W, lane, d, d_hi, hi_rows);
@@ -1462,7 +1546,10 @@ __global__ __launch_bounds__(NW * WAVE, MIN_WAVES_PER_EU) void mi_cls_kernel(KAr
 				n_off = a.off[p2];
 				n_len = a.len[p2];
 			}
-			d_hi = load_window(rs, d_off, d_len, lane, d);
+			// no loads for a tile past the end (its registers would be
+			// waited for before reuse after the loop)
+			if (tile + tstride < nt)
+				d_hi = load_window(rs, d_off, d_len, lane, d, want_hi, d_win);
 		}
 		wave_lds_sync();
 #ifdef DIAG_STAGEONLY
@@ -1481,6 +1568,7 @@ __global__ __launch_bounds__(NW * WAVE, MIN_WAVES_PER_EU) void mi_cls_kernel(KAr
 		k.w = W + lane;
 		k.g = a.pkts + my_off;
 		k.len = my_len;
+		k.win = my_win;
 
 		STAMP(1);   // next tile's loads issued
 		Parsed p;
@@ -1499,6 +1587,20 @@ __global__ __launch_bounds__(NW * WAVE, MIN_WAVES_PER_EU) void mi_cls_kernel(KAr
 				l4_chksum(k, p, a.opt, rs, my_off);
 		}
 		const Fields x = fields_of(k, p);
+		{
+			// bytes this tile's lanes use: the parse's L3 / L4 headers and the
+			// program's fields (conservative: gates ignored)
+			const uint32_t l4h = (p.flags & F_TCP) ? 13u : ((p.flags & F_UDP) ? 6u : 0u);
+			uint32_t need = p_frend;
+			need = max(need, p.l3 != 0xFFFFu ? p.l3 + max(p_l3end, (p.flags & F_IPV6) ? 40u : 20u) : 0u);
+			need = max(need, p.l4 != 0xFFFFu ? p.l4 + max(p_l4end, l4h) : 0u);
+#ifdef DIAG_FORCE_HI
+			want_hi = true;
+#else
+			want_hi = a.opt != 0u || __ballot(valid && my_len > 64u && need > 64u) != 0ull;
+#endif
+			saw_hi = saw_hi || want_hi;
+		}
 #ifdef DIAG_PARSEONLY
 		if (valid) {
 			uint4 rec;
@@ -1644,8 +1746,14 @@ __global__ __launch_bounds__(NW * WAVE, MIN_WAVES_PER_EU) void mi_cls_kernel(KAr
 		prev_valid = valid;
 		STAMP(4);   // outcome computed, record stored
 	}
+	STAMP(7);   // loop left
 	if (prev_valid)
 		*(uint4 *)(a.out + prev_pi) = prev_rec;
+	// the waves of block 0 are the sample that sets the hint: stores to one
+	// address serialise, so never one per wave
+	if (saw_hi && a.hint && lane == 0 && blockIdx.x == 0)
+		*a.hint = a.seq;
+	STAMP(6);   // last record issued
 #ifdef DIAG_STAMPS
 	if (lane == 0 && a.diag) {
 		for (int i = 0; i < NSTAMP; ++i)
@@ -1673,6 +1781,8 @@ struct mi_cls_ctx {
 	int wpb;                 // forced waves per block (MI_CLS_WPB at load), 0 = auto
 	uint32_t opt;            // pktin options (mi_cls_pktin_opt_set)
 	unsigned long long *d_stats;
+	uint32_t *d_hint;        // window hint word (KArgs.hint)
+	uint32_t seq;            // launches so far
 	int stats_on;
 	uint32_t stats_mask[8];
 	int num_cu;
@@ -1719,7 +1829,9 @@ extern "C" int mi_cls_ctx_create(int device, mi_cls_ctx_t **out)
 	else
 		c->num_cu = 256;
 	if (hipMalloc((void **)&c->d_stats, MAX_STATS_COS * sizeof(unsigned long long)) != hipSuccess ||
-	    hipMemset(c->d_stats, 0, MAX_STATS_COS * sizeof(unsigned long long)) != hipSuccess) {
+	    hipMemset(c->d_stats, 0, MAX_STATS_COS * sizeof(unsigned long long)) != hipSuccess ||
+	    hipMalloc((void **)&c->d_hint, sizeof(uint32_t)) != hipSuccess ||
+	    hipMemset(c->d_hint, 0, sizeof(uint32_t)) != hipSuccess) {
 		free(c);
 		(void)hipSetDevice(cur);
 		return -ENOMEM;
@@ -1738,6 +1850,8 @@ extern "C" int mi_cls_ctx_destroy(mi_cls_ctx_t *c)
 		(void)hipFree(c->d_dev);
 	if (c->d_stats)
 		(void)hipFree(c->d_stats);
+	if (c->d_hint)
+		(void)hipFree(c->d_hint);
 	if (c->stream)
 		(void)hipStreamDestroy(c->stream);
 	(void)hipFree(c->d_pk);
@@ -1855,55 +1969,85 @@ static uint32_t host_bv_fold(const Key4 &k)
 	return h ^ (h >> 15);
 }
 
-static uint32_t host_bucket(uint32_t fold, uint32_t mult, uint32_t nb)
+// bv_bucket() on the host: x = key word or fold, 2^kb buckets
+static uint32_t host_bucket(uint32_t x, uint32_t mult, uint32_t kb)
 {
-	return (uint32_t)(((uint64_t)(uint32_t)(fold * mult) * nb) >> 32);
+	const uint32_t y = (x ^ (x >> 16)) & 0xFFFFFFu;
+	return (uint32_t)(y * (uint64_t)(mult & 0xFFFFFFu)) >> (32u - kb);
 }
 
-// Two-choice cuckoo table over `keys`: every key sits in slot s1 or s2 (a
-// lookup reads both at once, no probe loop).  Returns the slot of every key
-// and the slot count / multipliers used (load factor <= 45 %).
-static bool cuckoo_place(const std::vector<Key4> &keys, uint32_t &ns, uint32_t &m1, uint32_t &m2,
-			 std::vector<uint32_t> &slot_of)
+// Two-choice cuckoo table over `keys`: every key sits in a slot of bucket
+// b1 or b2 (a lookup reads both buckets at once, no probe loop).  bsz slots
+// per bucket: 2 for one-word keys (a 16-B bucket, load <= 80 %), 1 for
+// longer keys (load <= 45 %).  Returns the slot (bucket * bsz + j) of every
+// key, the bucket count and the multipliers used.
+static bool cuckoo_place(const std::vector<Key4> &keys, uint32_t nk, uint32_t bsz, uint32_t &kb,
+			 uint32_t &m1, uint32_t &m2, std::vector<uint32_t> &slot_of)
 {
 	const uint32_t n = (uint32_t)keys.size();
 	std::vector<uint32_t> fold(n);
 	for (uint32_t i = 0; i < n; ++i)
-		fold[i] = host_bv_fold(keys[i]);
-	ns = (n * 20 + 8) / 9 + 2;
+		fold[i] = nk == 1 ? keys[i][0] : host_bv_fold(keys[i]);
+	// 2^kb buckets: load <= 80 % with 2-slot buckets, <= 45 % otherwise
+	const uint64_t need = bsz == 2 ? ((uint64_t)n * 5 + 7) / 8 : ((uint64_t)n * 20 + 8) / 9;
+	kb = 1;
+	while ((1ull << kb) < need)
+		++kb;
 	uint64_t rng = 0x9E3779B97F4A7C15ull ^ ((uint64_t)n << 17);
-	for (int grow = 0; grow < 8; ++grow, ns += ns / 4 + 1) {
-		for (int attempt = 0; attempt < 32; ++attempt) {
+	for (int grow = 0; grow < 4 && kb <= 20; ++grow, ++kb) {
+		const uint32_t nb = 1u << kb;
+		for (int attempt = 0; attempt < 64; ++attempt) {
 			rng ^= rng << 13; rng ^= rng >> 7; rng ^= rng << 17;
-			m1 = (uint32_t)rng | 1u;
+			m1 = ((uint32_t)rng & 0xFFFFFFu) | 1u;
 			rng ^= rng << 13; rng ^= rng >> 7; rng ^= rng << 17;
-			m2 = (uint32_t)(rng >> 32) | 1u;
-			std::vector<int32_t> occ(ns, -1);
+			m2 = ((uint32_t)(rng >> 32) & 0xFFFFFFu) | 1u;
+			std::vector<int32_t> occ((size_t)nb * bsz, -1);
 			slot_of.assign(n, 0);
 			bool ok = true;
 			for (uint32_t i = 0; i < n && ok; ++i) {
-				uint32_t cur = i, pos = host_bucket(fold[i], m1, ns);
+				uint32_t cur = i, b = host_bucket(fold[i], m1, kb);
 				for (int kick = 0;; ++kick) {
-					if (occ[pos] < 0) {
-						occ[pos] = (int32_t)cur;
-						slot_of[cur] = pos;
+					// a free slot in either bucket of `cur`
+					const uint32_t c1 = host_bucket(fold[cur], m1, kb);
+					const uint32_t c2 = host_bucket(fold[cur], m2, kb);
+					int32_t fs = -1;
+					for (uint32_t bb : { c1, c2 })
+						for (uint32_t j = 0; j < bsz && fs < 0; ++j)
+							if (occ[(size_t)bb * bsz + j] < 0)
+								fs = (int32_t)(bb * bsz + j);
+					if (fs >= 0) {
+						occ[fs] = (int32_t)cur;
+						slot_of[cur] = (uint32_t)fs;
 						break;
 					}
-					if (kick > 300) {
+					if (kick > 500) {
 						ok = false;
 						break;
 					}
-					const uint32_t ev = (uint32_t)occ[pos];
-					occ[pos] = (int32_t)cur;
-					slot_of[cur] = pos;
-					const uint32_t a1 = host_bucket(fold[ev], m1, ns);
-					const uint32_t a2 = host_bucket(fold[ev], m2, ns);
-					pos = a1 == pos ? a2 : a1;
+					// evict a pseudo-random slot of bucket b (alternating buckets)
+					rng ^= rng << 13; rng ^= rng >> 7; rng ^= rng << 17;
+					const uint32_t sl = b * bsz + (uint32_t)(rng % bsz);
+					const uint32_t ev = (uint32_t)occ[sl];
+					occ[sl] = (int32_t)cur;
+					slot_of[cur] = sl;
 					cur = ev;
+					const uint32_t e1 = host_bucket(fold[ev], m1, kb);
+					const uint32_t e2 = host_bucket(fold[ev], m2, kb);
+					b = e1 == b ? e2 : e1;
 				}
 			}
-			if (ok)
-				return true;
+			if (ok) {
+				// every key must sit in one of its two buckets
+				for (uint32_t i = 0; i < n && ok; ++i) {
+					const uint32_t bk = slot_of[i] / bsz;
+					ok = occ[slot_of[i]] == (int32_t)i &&
+					     (bk == host_bucket(fold[i], m1, kb) ||
+					      bk == host_bucket(fold[i], m2, kb));
+				}
+				if (ok)
+					return true;
+				fprintf(stderr, "mi_cls: cuckoo placement self-check failed\n");
+			}
 		}
 	}
 	return false;
@@ -1935,7 +2079,34 @@ static bool class_of(const mi_term_t &t, ClassKey &ck)
 	}
 	for (uint32_t i = 0; i < 4; ++i)
 		ck.mask[i] = i < ck.nkey ? eff_mask(t, i) : 0;
+	// UDP and TCP port terms read the same bytes (the raw port word at l4)
+	// under different gates: one class for both, the protocol carried in
+	// two key bits the mask leaves free (tag 1 UDP, 2 TCP; port masks are
+	// <= 16 bits, so bits tp, tp+1 exist), so a packet's key holds its
+	// protocol and one lookup serves rules of either kind.
+	static const bool no_merge = getenv("MI_CLS_NO_PORTMERGE") != nullptr;   // A/B, tests
+	if (!no_merge && (t.kind == MI_K_UDP_DPORT || t.kind == MI_K_TCP_DPORT ||
+			  t.kind == MI_K_UDP_SPORT || t.kind == MI_K_TCP_SPORT)) {
+		uint32_t tp = 0;
+		while (tp < 31 && ((ck.mask[0] >> tp) & 3u))
+			++tp;
+		if (tp < 31) {
+			ck.kind = K_L4PORT;
+			ck.offset = tp;
+		}
+	}
 	return true;
+}
+
+// value words a term requires of its class (the tag of a merged port class)
+static Key4 class_value(const mi_term_t &t, const ClassKey &ck)
+{
+	Key4 v = { 0, 0, 0, 0 };
+	for (uint32_t i = 0; i < ck.nkey; ++i)
+		v[i] = t.value[i];
+	if (ck.kind == K_L4PORT)
+		v[0] |= (t.kind == MI_K_UDP_DPORT || t.kind == MI_K_UDP_SPORT ? 1u : 2u) << ck.offset;
+	return v;
 }
 
 // Build the classification block of one CoS into `blk` (word offsets are
@@ -2002,9 +2173,7 @@ static bool build_bv(const mi_cos_t *cs, const mi_rule_t *rs, const mi_term_t *t
 				continue;
 			}
 			const uint32_t c = cls[ck];
-			Key4 v = { 0, 0, 0, 0 };
-			for (uint32_t i = 0; i < ck.nkey; ++i)
-				v[i] = tm.value[i];
+			const Key4 v = class_value(tm, ck);
 			if (((tmask[r] >> c) & 1u) && want[r][c] != v)
 				ok = false;   // two terms of one class with different values
 			tmask[r] |= 1u << c;
@@ -2046,26 +2215,34 @@ static bool build_bv(const mi_cos_t *cs, const mi_rule_t *rs, const mi_term_t *t
 		blk.push_back((rs[r].dst_cos & 0xffu) | (cs[rs[r].dst_cos].num_rules == 0 ? 0x100u : 0u) |
 			      ((uint32_t)rs[r].mark << 16));
 	std::vector<std::vector<std::vector<uint32_t>>> lists(ncls);   // [class][key id] -> rules
-	// wide rows: nw words each, deduplicated, appended to the block; a row's
-	// value is its hot-region word index (non-zero: the CoS table comes first)
+	// wide rows: 8 words each (zero past the rule count), deduplicated.  Every
+	// row id is assigned before the layout is emitted (mode 3 below): rows
+	// are stored as two arrays of 4-word halves, so a row's value is the
+	// hot-region word index of its first half and the second half is
+	// blk[7] words further (16-B aligned; consecutive rows 16 B apart)
 	const uint32_t nw = (nrules + 31u) / 32u;
-	std::map<std::vector<uint32_t>, uint32_t> row_at;
-	auto put_row = [&](const std::vector<uint32_t> &row) -> uint32_t {
-		auto it = row_at.find(row);
-		if (it != row_at.end())
-			return it->second;
-		const uint32_t at = base + (uint32_t)blk.size();
-		blk.insert(blk.end(), row.begin(), row.end());
-		row_at[row] = at;
-		return at;
-	};
 	auto wide_row = [&](uint32_t c, const Key4 *v) {
-		std::vector<uint32_t> w(BV_WIDE_WORDS, 0u);   // zero past the rule count
+		std::vector<uint32_t> w(BV_WIDE_WORDS, 0u);
 		for (uint32_t r = 0; r < nrules; ++r)
 			if (holds_class(r, c, v))
 				w[r / 32u] |= 1u << (r % 32u);
 		return w;
 	};
+	std::map<std::vector<uint32_t>, uint32_t> row_id;
+	std::vector<const std::vector<uint32_t> *> rows;
+	auto get_row = [&](const std::vector<uint32_t> &row) -> uint32_t {
+		auto it = row_id.find(row);
+		if (it != row_id.end())
+			return it->second;
+		const uint32_t id = (uint32_t)rows.size();
+		auto ins = row_id.emplace(row, id).first;
+		rows.push_back(&ins->first);
+		return id;
+	};
+	std::vector<uint32_t> miss_id(ncls, 0);
+	std::vector<std::vector<uint32_t>> key_row(ncls);
+	uint32_t rows_at = 0;   // block-relative index of the first-halves array
+	auto align4 = [&]() { while (blk.size() & 3u) blk.push_back(0); };
 	if (mode == 2u) {
 		uint32_t aw = 0;
 		for (uint32_t r = 0; r < nrules; ++r)
@@ -2080,6 +2257,18 @@ static bool build_bv(const mi_cos_t *cs, const mi_rule_t *rs, const mi_term_t *t
 				aw |= (uint32_t)alive[32u * i + j] << j;
 			blk.push_back(aw);
 		}
+		for (uint32_t c = 0; c < ncls; ++c) {
+			miss_id[c] = get_row(wide_row(c, nullptr));
+			for (auto &kv : kid[c])
+				key_row[c].push_back(get_row(wide_row(c, &kv.first)));
+		}
+		align4();
+		rows_at = (uint32_t)blk.size();
+		const uint32_t R = (uint32_t)rows.size();
+		blk[7] = 4u * R;
+		for (uint32_t h = 0; h < 2; ++h)
+			for (uint32_t j = 0; j < R; ++j)
+				blk.insert(blk.end(), rows[j]->begin() + 4 * h, rows[j]->begin() + 4 * h + 4);
 	} else if (mode == 1u) {
 		const uint32_t RW = 1u + (ncls + 1u) / 2u;
 		blk[4] = base + (uint32_t)blk.size();
@@ -2127,23 +2316,25 @@ static bool build_bv(const mi_cos_t *cs, const mi_rule_t *rs, const mi_term_t *t
 		std::vector<Key4> keys;
 		for (auto &kv : kid[c])
 			keys.push_back(kv.first);
-		uint32_t nb = 4, m1 = 1, m2 = 3;
+		uint32_t kb = 1, m1 = 1, m2 = 3;
 		std::vector<uint32_t> slot_of;
-		if (!cuckoo_place(keys, nb, m1, m2, slot_of))
+		// one-word keys: 2-slot buckets of 16 B; longer keys: 1 slot per bucket
+		const uint32_t bsz = ck.nkey == 1 ? 2u : 1u;
+		if (!cuckoo_place(keys, ck.nkey, bsz, kb, m1, m2, slot_of))
 			return false;
+		const uint32_t nb = 1u << kb;
 		const uint32_t cbase = 8 + BV_CLS_WORDS * c;
 		const uint32_t SW = ck.nkey + 1u;   // slot: key words, value
 		blk[cbase + 0] = ck.kind;
 		blk[cbase + 1] = ck.nkey;
-		// (put_row grows blk: compute before indexing it)
 		const uint32_t miss = mode == 0u ? first_live(c, nullptr)
-			: (mode == 2u ? row_of(c, nullptr) : (mode == 3u ? put_row(wide_row(c, nullptr)) : 0u));
+			: (mode == 2u ? row_of(c, nullptr) : (mode == 3u ? base + rows_at + 4u * miss_id[c] : 0u));
 		blk[cbase + 2] = miss;
 		blk[cbase + 3] = ck.offset;
 		blk[cbase + 4] = ck.size;
 		for (int i = 0; i < 4; ++i)
 			blk[cbase + 5 + i] = ck.mask[i];
-		blk[cbase + 9] = nb;
+		blk[cbase + 9] = kb;
 		blk[cbase + 11] = m1;
 		blk[cbase + 12] = m2;
 		{
@@ -2159,15 +2350,17 @@ static bool build_bv(const mi_cos_t *cs, const mi_rule_t *rs, const mi_term_t *t
 				: (d.altf == F_IPV4 ? 2u : (d.altf == F_AH ? 3u : 0u));
 			const uint32_t fl = (special ? BVF_SPECIAL : 0u) |
 				((ck.kind == MI_K_CUSTOM_FRAME || ck.kind == MI_K_CUSTOM_L3) ? BVF_CUSTOM : 0u) |
-				(ck.kind == MI_K_CUSTOM_L3 ? BVF_L3 : 0u);
+				(ck.kind == MI_K_CUSTOM_L3 ? BVF_L3 : 0u) | (ck.kind == K_L4PORT ? BVF_TAG : 0u);
 			blk[cbase + BVC_AO] = d.add | (d.alt << 16);
 			blk[cbase + BVC_DESC] = (gate & 0xffffffu) | (d.base << 24) | (ac << 26) | (fl << 28);
 		}
+		if (bsz == 2)
+			align4();   // 16-B buckets
 		const uint32_t tbl_off = (uint32_t)blk.size();
 		blk[cbase + 10] = base + tbl_off;
 		// empty slots keep key words 0 and value 0: a miss (every stored
 		// value is non-zero)
-		blk.resize(blk.size() + (size_t)nb * SW, 0);
+		blk.resize(blk.size() + (size_t)nb * bsz * SW, 0);
 		uint32_t list_at = 0;
 		if (mode == 1u) {
 			blk[cbase + 13] = base + (uint32_t)blk.size();
@@ -2190,7 +2383,7 @@ static bool build_bv(const mi_cos_t *cs, const mi_rule_t *rs, const mi_term_t *t
 			} else if (mode == 2u) {
 				val = row_of(c, &keys[i]);   // non-zero: the key's own rules
 			} else if (mode == 3u) {
-				val = put_row(wide_row(c, &keys[i]));   // word index, non-zero
+				val = base + rows_at + 4u * key_row[c][i];   // word index, non-zero
 			} else {
 				const uint32_t id = kid[c][keys[i]];
 				uint32_t off = 0;
@@ -2227,6 +2420,8 @@ static int assemble(const void *tbl, uint32_t **out, size_t *out_words)
 			if (!cs[s].valid || cs[s].num_rules == 0)
 				continue;
 			std::vector<uint32_t> blk;
+			while (hot.size() & 3u)   // blocks start 16-B aligned (16-B row / bucket reads)
+				hot.push_back(0);
 			const uint32_t base = (uint32_t)hot.size();
 			if (build_bv(cs, rs + cs[s].rule_begin, ts, cs[s].num_rules, base, blk)) {
 				hot[COS_WORDS * s + C_BV] = base;
@@ -2249,6 +2444,39 @@ static int assemble(const void *tbl, uint32_t **out, size_t *out_words)
 	w[DH_HOT_OFF] = hot_off;
 	w[DH_HOT_WORDS] = (uint32_t)hot.size();
 	w[DH_PROG_OFF] = (uint32_t)prog_off;
+	{
+		// furthest bytes the terms read, per base (window predictor only:
+		// correctness never depends on these)
+		uint32_t end[3] = { 0, 0, 0 };
+		for (uint32_t i = 0; i < h->num_terms; ++i) {
+			const mi_term_t &t = ts[i];
+			uint32_t base = FB_FRAME, e = 0;
+			switch (t.kind) {
+			case MI_K_LEN: case MI_K_NEVER: case MI_K_ALWAYS:
+				break;
+			case MI_K_PCP0: e = 16; break;
+			case MI_K_DSCP: base = FB_L3; e = 4; break;
+			case MI_K_CUSTOM_FRAME: e = t.offset + t.size + 4u; break;
+			case MI_K_CUSTOM_L3: base = FB_L3; e = t.offset + t.size + 4u; break;
+			default: {
+				const FDesc d = fdesc(t.kind, 0);
+				const uint32_t nw = (t.kind == MI_K_SIP6 || t.kind == MI_K_DIP6) ? 4u
+					: (t.kind == MI_K_DMAC ? 2u : 1u);
+				base = d.base;
+				e = std::max(d.add, d.alt) + 4u * nw;
+			}
+			}
+			end[base] = std::max(end[base], std::min(e, 0xFFFFu));
+		}
+		for (uint32_t s = 0; s < h->num_cos; ++s)
+			if (cs[s].num_queue > 1) {   // Toeplitz tuple (rss_hash)
+				end[FB_L3] = std::max(end[FB_L3], 40u);
+				end[FB_L4] = std::max(end[FB_L4], 4u);
+			}
+		w[DH_FREND] = end[FB_FRAME];
+		w[DH_L3END] = end[FB_L3];
+		w[DH_L4END] = end[FB_L4];
+	}
 	std::vector<uint32_t> ext;
 	const size_t ext_base = (size_t)h->num_rules * REC_WORDS;
 	for (uint32_t r = 0; r < h->num_rules; ++r) {
@@ -2281,6 +2509,43 @@ static int assemble(const void *tbl, uint32_t **out, size_t *out_words)
 	memcpy(o, w.data(), w.size() * sizeof(uint32_t));
 	*out = o;
 	*out_words = w.size();
+	return 0;
+}
+
+// Host-only introspection of the device encoding a table assembles into (no
+// device needed): info[0] total words, [1] hot-region words, [2] CoS with a
+// classification block, [3..6] blocks per mode (direct, candidate, bitmap,
+// wide), [7] 1 if the program is a tree (DIV kernel).  Tests and tools use it
+// to check the engine choice on the CPU.
+extern "C" int mi_cls_program_info(const void *tbl, size_t bytes, uint32_t *info, uint32_t n)
+{
+	if (!info || n < 8)
+		return -EINVAL;
+	int rc = validate_tbl(tbl, bytes);
+	if (rc)
+		return rc;
+	uint32_t *w = nullptr;
+	size_t words = 0;
+	rc = assemble(tbl, &w, &words);
+	if (rc)
+		return rc;
+	memset(info, 0, n * sizeof(uint32_t));
+	info[0] = (uint32_t)words;
+	info[1] = w[DH_HOT_WORDS];
+	const mi_tbl_hdr_t *th = (const mi_tbl_hdr_t *)tbl;
+	const uint32_t *hot = w + w[DH_HOT_OFF];
+	for (uint32_t s = 0; s < th->num_cos; ++s) {
+		const uint32_t bv = hot[COS_WORDS * s + C_BV];
+		if (bv) {
+			info[2]++;
+			info[3 + (hot[bv] & 3u)]++;
+		}
+	}
+	const mi_cos_t *tc = (const mi_cos_t *)((const uint8_t *)tbl + th->cos_off);
+	const mi_rule_t *tr = (const mi_rule_t *)((const uint8_t *)tbl + th->rule_off);
+	for (uint32_t r = 0; r < th->num_rules && !info[7]; ++r)
+		info[7] = tc[tr[r].dst_cos].num_rules != 0;
+	free(w);
 	return 0;
 }
 
@@ -2370,6 +2635,10 @@ extern "C" int mi_cls_classify(mi_cls_ctx_t *c, const uint8_t *pkts, const uint3
 	a.stats = c->stats_on ? c->d_stats : nullptr;
 	a.diag = nullptr;
 	a.opt = c->opt;
+	a.hint = c->d_hint;
+	a.seq = ++c->seq;
+	if (a.seq == 0u)   // wrapped: the hint word may equal seq - 1 by accident
+		a.seq = c->seq = 2u;
 #ifdef DIAG_STAMPS
 	static unsigned long long *d_diag = nullptr;
 	if (!d_diag)
@@ -2398,7 +2667,7 @@ extern "C" int mi_cls_classify(mi_cls_ctx_t *c, const uint8_t *pkts, const uint3
 	// forces a shape (A/B runs).
 	const int wpb_env = c->wpb;
 	const size_t LDS_CU = 160u * 1024u;
-	const size_t hot_bytes = (size_t)c->hot_words * sizeof(uint32_t);
+	const size_t hot_bytes = (((size_t)c->hot_words + 3u) & ~(size_t)3u) * sizeof(uint32_t);
 	const size_t st4 = sizeof(uint32_t) * (4 * RS * WROWS + MAX_STATS_COS + 256);
 	const size_t st16 = sizeof(uint32_t) * (16 * RS * WROWS + MAX_STATS_COS + 256);
 	const bool fits16 = st16 + hot_bytes <= LDS_CU;
@@ -2456,7 +2725,7 @@ extern "C" int mi_cls_classify(mi_cls_ctx_t *c, const uint8_t *pkts, const uint3
 		(void)hipStreamSynchronize((hipStream_t)stream);
 		(void)hipMemcpy(h, d_diag, sizeof(h), hipMemcpyDeviceToHost);
 		fprintf(stderr, "DIAG waves=%llu cycles/wave:", h[8]);
-		for (int i = 0; i < 5; ++i)
+		for (int i = 0; i < 8; ++i)
 			fprintf(stderr, " p%d=%.0f", i, (double)h[i] / (double)(h[8] ? h[8] : 1));
 		fprintf(stderr, "\n");
 	}
