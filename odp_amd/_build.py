@@ -55,9 +55,26 @@ def build(force: bool = False, out_dir: str = PKG, defines=()) -> list[str]:
                       os.path.join(INC, "odp", "helper", "odph_api.h"),
                       os.path.join(SRC, "odp_rt_internal.h")]
     built = []
-    if force or defines or _stale(mi_so, [mi_src] + hdrs):
-        _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-              "-Wall", "-I", INC] + [f"-D{d}" for d in defines] + ["-o", mi_so, mi_src])
+    mi_hdr = os.path.join(SRC, "mi_cls_dev.h")
+    k_srcs = [os.path.join(SRC, f"mi_cls_k{w}.hip") for w in (4, 8, 12, 16)]
+    if force or defines or _stale(mi_so, [mi_src, mi_hdr] + k_srcs + hdrs):
+        # one translation unit per block shape + the host code, compiled in
+        # parallel (the kernel instantiations dominate the build time)
+        import concurrent.futures as cf
+        import tempfile
+        tmp = tempfile.mkdtemp(prefix="mi_cls_obj_")
+        flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-I", INC,
+                 "-I", SRC] + [f"-D{d}" for d in defines]
+        objs = []
+        jobs = []
+        for src in [mi_src] + k_srcs:
+            obj = os.path.join(tmp, os.path.basename(src) + ".o")
+            objs.append(obj)
+            jobs.append([HIPCC] + flags + ["-c", "-o", obj, src])
+        with cf.ThreadPoolExecutor(max_workers=len(jobs)) as ex:
+            list(ex.map(_run, jobs))
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", mi_so] + objs)
+        shutil.rmtree(tmp, ignore_errors=True)
         built.append(mi_so)
     if force or _stale(odp_so, odp_srcs + [mi_so] + rt_hdrs):
         _run(["gcc", "-O2", "-std=gnu11", "-Wall", "-Wextra", "-fPIC", "-shared", "-I", INC,

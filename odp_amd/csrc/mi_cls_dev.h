@@ -1,0 +1,1795 @@
+// mi_cls_dev.h -- device side of the gfx950 (MI355X / CDNA4) packet parse +
+// PMR classify path: packet byte access, the parsers, the classification
+// engines, the device rule-program encoding and the mi_cls_kernel template.
+// Included by the kernel translation units (mi_cls_k<NW>.hip, one block
+// shape each, compiled in parallel) and by the host code in mi_cls.hip (for
+// the encoding constants and fdesc()).
+//
+// What it replaces (reference, platform/linux-generic/):
+//   pktio/loop.c:283-339        per-packet parse + classify inside loopback_recv
+//   odp_parse.c:23-488          _odp_parse_eth / parse_ipv4 / parse_ipv6 / parse_tcp
+//                               / parse_udp / parse_sctp / _odp_packet_parse_common_l3_l4
+//   odp_classification.c:931-1515   verify_pmr and the per-term verifiers
+//   odp_classification.c:1624-1771  match_pmr_cos / cls_select_cos / _odp_cls_classify_packet
+//   odp_classification.c:395-405, 1773-1839 + protocols/thash.h:82-99  hash-queue pick
+//
+// Design (MI355X-first, not a translation; DESIGN.md has the details):
+//   * one wavefront owns 64 consecutive packets (a tile, one packet per lane)
+//     and loops over its tiles with the next tile's header loads in flight;
+//   * the first 64 B (96 B when the frames need them) of every packet are
+//     loaded cooperatively (4 lanes per packet, 16-B buffer loads, so one
+//     instruction covers 16 back-to-back headers) and stored dword-major,
+//     lane-minor into the wave's LDS window, where each lane reads any byte
+//     offset of its own frame without bank conflicts; bytes past the window
+//     come from HBM, bytes past the frame read 0;
+//   * parse_fast (selects, wave-uniform skips) covers the common header
+//     shapes, parse_packet restates every branch of odp_parse.c;
+//   * classification: per CoS a block of key classes looked up in two-choice
+//     cuckoo tables (16-B buckets), combined by the direct / bitmap / wide
+//     bitmap / candidate engines; the CoS tree is descended one hop per
+//     round, per-lane blocks when lanes sit on different CoS.  No MFMA:
+//     this is parse-and-compare.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <errno.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "mi_cls.h"
+
+#include <algorithm>
+#include <type_traits>
+#include <array>
+#include <map>
+#include <vector>
+
+#define WAVE 64
+#ifndef WIN
+#define WIN 96             // staged header window, bytes (96 or 128)
+#endif
+#define WROWS (WIN / 4 + 3)     // LDS dword rows per wave window (+3 zero rows)
+#define RS 66                   // LDS row stride of a window, dwords (see load_window)
+#define NPIECE (WIN / 16)       // 16-B pieces per window
+#ifndef MIN_WAVES_PER_EU
+#define MIN_WAVES_PER_EU 4
+#endif
+#ifndef LOAD_AUX
+#define LOAD_AUX 2          // cache policy of the packet-window loads: nt (read once)
+#endif
+#ifndef PREFETCH
+#define PREFETCH 1          // software-pipeline the next tile's loads
+#endif
+#define MAX_STATS_COS 256
+
+// ---------------------------------------------------------------- flags
+// input_flags bits: include/odp/api/plat/packet_inline_types.h:66-107
+#define F_CLS_MARK  (1u << 0)
+#define F_L2        (1u << 3)
+#define F_L3        (1u << 4)
+#define F_L4        (1u << 5)
+#define F_ETH       (1u << 6)
+#define F_ETH_BCAST (1u << 7)
+#define F_ETH_MCAST (1u << 8)
+#define F_JUMBO     (1u << 9)
+#define F_VLAN      (1u << 10)
+#define F_QINQ      (1u << 11)
+#define F_ARP       (1u << 12)
+#define F_IPV4      (1u << 13)
+#define F_IPV6      (1u << 14)
+#define F_IP_BCAST  (1u << 15)
+#define F_IP_MCAST  (1u << 16)
+#define F_IPFRAG    (1u << 17)
+#define F_IPOPT     (1u << 18)
+#define F_IPSEC     (1u << 19)
+#define F_AH        (1u << 20)
+#define F_ESP       (1u << 21)
+#define F_UDP       (1u << 22)
+#define F_TCP       (1u << 23)
+#define F_SCTP      (1u << 24)
+#define F_ICMP      (1u << 25)
+#define F_NO_NEXT   (1u << 26)
+// error group bits (flags.all.error, packet_inline_types.h:152-165)
+#define E_SNAP 1u
+#define E_IP   2u
+#define E_TCP  8u
+#define E_UDP  16u
+#define E_SCTP 32u
+#define E_L3CK 4u           // l3_chksum_err
+#define E_L4CK 64u          // l4_chksum_err
+#define F_L3CK_DONE (1u << 30)   // input_flags.l3_chksum_done
+#define F_L4CK_DONE (1u << 31)   // input_flags.l4_chksum_done
+// pktin options: odp_pktin_config_opt_t.all_bits (include/odp_rt.h)
+#define OPT_IPV4_CK (1u << 2)
+#define OPT_UDP_CK (1u << 3)
+#define OPT_TCP_CK (1u << 4)
+#define OPT_SCTP_CK (1u << 5)
+#define OPT_DROP_V4 (1u << 6)
+#define OPT_DROP_V6 (1u << 7)
+#define OPT_DROP_UDP (1u << 8)
+#define OPT_DROP_TCP (1u << 9)
+#define OPT_DROP_SCTP (1u << 10)
+#define OPT_L4_CK (OPT_UDP_CK | OPT_TCP_CK | OPT_SCTP_CK)
+
+// ------------------------------------------------------- packet byte access
+// The LDS window of a wave is dword-major, lane-minor: dword i of lane l's
+// packet lives at W[i * RS + l] (RS = 66).  Any per-lane byte offset then
+// reads conflict-free (lane l of row i hits bank 2i + l mod 32), whatever the
+// packets' header layouts.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+struct Pkt {
+	const uint32_t *w;      // &W[lane]
+	const uint8_t *g;       // packet start in HBM
+	uint32_t len;           // frame_len
+	uint32_t win;           // bytes of the frame staged in LDS this tile (64 or WIN;
+	                        // wave-uniform): bytes [0, min(len, win)) are in
+	                        // the window, bytes past the frame read 0
+};
+
+// One byte; past the staged window it comes from HBM (the general parser and
+// the rare far field), past the frame it is 0.
+__device__ __forceinline__ uint32_t rb(const Pkt &k, uint32_t o)
+{
+	if (o < k.win)
+		return (k.w[(o >> 2) * RS] >> ((o & 3u) * 8u)) & 0xffu;
+	return o < k.len ? (uint32_t)k.g[o] : 0u;
+}
+
+// 4 bytes starting at byte offset o, little-endian (== the reference's raw
+// load).  The LDS read is unconditional (row index clamped into the window
+// and its zero rows), so lanes do not diverge; a wave-uniform branch fixes up
+// the lanes whose 4 bytes reach past the staged window (bytes from HBM).
+__device__ __forceinline__ uint32_t r32(const Pkt &k, uint32_t o)
+{
+	const uint32_t i = min(o >> 2, (uint32_t)(WIN / 4 + 1));
+	uint32_t v = __builtin_amdgcn_alignbyte(k.w[(i + 1) * RS], k.w[i * RS], o & 3u);
+	const bool far = o + 4u > k.win;
+	if (__ballot(far) != 0ull) {
+		if (far)
+			v = rb(k, o) | (rb(k, o + 1) << 8) | (rb(k, o + 2) << 16) | (rb(k, o + 3) << 24);
+	}
+	return v;
+}
+
+__device__ __forceinline__ uint32_t r16(const Pkt &k, uint32_t o)
+{
+	return r32(k, o) & 0xffffu;
+}
+
+__device__ __forceinline__ uint32_t be16(const Pkt &k, uint32_t o)
+{
+	uint32_t v = r16(k, o);
+	return ((v & 0xffu) << 8) | (v >> 8);
+}
+
+__device__ __forceinline__ uint32_t be32(const Pkt &k, uint32_t o)
+{
+	return __builtin_bswap32(r32(k, o));
+}
+
+// ------------------------------------------------------------------ parse
+struct Parsed {
+	uint32_t flags;
+	uint32_t err;
+	uint32_t l3, l4;
+	int ret;                // 0 ok, 1 error flags, -1 drop
+	uint32_t udp_zero;      // input_flags.udp_chksum_zero (bit 32: not stored)
+};
+
+// one's-complement fold of a 64-bit partial sum (chksum_finalize,
+// include/odp_chksum_internal.h)
+__device__ __forceinline__ uint32_t ck_finalize(uint64_t s)
+{
+	s = (s >> 32) + (s & 0xffffffffull);
+	s = (s >> 16) + (s & 0xffffull);
+	return (uint32_t)((s >> 16) + s) & 0xffffu;
+}
+
+// _odp_parse_eth + _odp_packet_parse_common_l3_l4 (layer ALL) with the pktin
+// options `opt` (IPv4 header checksum, drop on IPv4/IPv6/UDP/TCP/SCTP
+// errors; the UDP zero-checksum rule of parse_udp), odp_parse.c:23-105,
+// 112-354, 362-488; contiguous packet so seg_end == frame_len.  The L4
+// checksums themselves are l4_chksum() below.
+__device__ __forceinline__ Parsed parse_packet(const Pkt &k, uint32_t opt)
+{
+	Parsed r;
+	const uint32_t len = k.len;
+	uint32_t f = F_L2 | F_ETH, err = 0, off = 14, ethtype, ip_proto = 255;
+	bool non_first = false;
+	r.udp_zero = 0;
+
+	r.l4 = 0xFFFFu;
+	uint32_t w0 = r32(k, 0), w1 = r32(k, 4);
+	if (len > 1514u)
+		f |= F_JUMBO;
+	if (w0 & 1u)
+		f |= F_ETH_MCAST;
+	if (w0 == 0xffffffffu && (w1 & 0xffffu) == 0xffffu)
+		f |= F_ETH_BCAST;
+	ethtype = be16(k, 12);
+	bool snap_err = false;
+	if (ethtype < 1514u) {
+		if (ethtype > len - 14u) {
+			err |= E_SNAP;
+			ethtype = 0;
+			snap_err = true;
+		} else {
+			ethtype = be16(k, 20);
+			off = 22;
+		}
+	}
+	if (!snap_err) {
+		if (ethtype == 0x88A8u) {
+			f |= F_QINQ | F_VLAN;
+			ethtype = be16(k, off + 2);
+			off += 4;
+		}
+		if (ethtype == 0x8100u) {
+			f |= F_VLAN;
+			ethtype = be16(k, off + 2);
+			off += 4;
+		}
+		if (off > len) {
+			f = F_L2;
+			ethtype = 0;
+		}
+	}
+
+	const uint32_t l3 = off;
+	r.l3 = l3;
+	f |= F_L3;
+	if (ethtype == 0x0800u) {
+		f |= F_IPV4;
+		uint32_t vi = rb(k, l3);
+		uint32_t ihl = vi & 0xfu;
+		uint32_t tot = be16(k, l3 + 2);
+		bool bad = ihl < 5u || (vi >> 4) != 4u || 20u > len - l3 || tot > len - l3;
+		if (!bad && (opt & OPT_IPV4_CK)) {
+			// odp_parse.c:134-141: header checksum over ihl * 4 bytes
+			f |= F_L3CK_DONE;
+			uint64_t s = 0;
+			for (uint32_t i = 0; i < ihl; ++i)
+				s += r32(k, l3 + 4u * i);
+			if (ck_finalize(s) != 0xffffu) {
+				err |= E_L3CK;
+				bad = true;
+			}
+		}
+		if (bad) {
+			err |= E_IP;
+			ip_proto = 0;
+		} else {
+			uint32_t frag = be16(k, l3 + 6);
+			uint32_t dst = be32(k, l3 + 16);
+			off = l3 + ihl * 4u;
+			if (ihl > 5u)
+				f |= F_IPOPT;
+			if (frag & 0x3fffu) {
+				f |= F_IPFRAG;
+				non_first = (frag & 0x1fffu) != 0;
+			}
+			if (dst == 0xffffffffu)
+				f |= F_IP_BCAST;
+			if ((dst >> 28) == 0xeu)
+				f |= F_IP_MCAST;
+			ip_proto = rb(k, l3 + 9);
+			r.l4 = off;
+		}
+	} else if (ethtype == 0x86DDu) {
+		f |= F_IPV6;
+		uint32_t plen = be16(k, l3 + 4);
+		if ((rb(k, l3) >> 4) != 6u || 40u > len - l3 || plen + 40u > len - l3) {
+			err |= E_IP;
+			ip_proto = 0;
+		} else {
+			if (rb(k, l3 + 24) == 0xffu)
+				f |= F_IP_MCAST;
+			off = l3 + 40;
+			uint32_t nh = rb(k, l3 + 6);
+			if (nh == 0u || nh == 43u) {
+				uint32_t nxt;
+				f |= F_IPOPT;
+				do {
+					uint32_t ext = off;
+					off += 8u + rb(k, ext + 1) * 8u;
+					nxt = rb(k, ext);
+				} while ((nxt == 0u || nxt == 43u) && off < len);
+				if (off >= l3 + plen) {
+					err |= E_IP;
+					ip_proto = 0;
+				} else {
+					if (nxt == 44u)
+						f |= F_IPFRAG;
+					ip_proto = nxt;
+					r.l4 = off;
+				}
+			} else {
+				if (nh == 44u)
+					f |= F_IPOPT | F_IPFRAG;
+				ip_proto = nh;
+				r.l4 = off;
+			}
+		}
+	} else if (ethtype == 0x0806u) {
+		f |= F_ARP;
+	} else {
+		f &= ~F_L3;
+	}
+	// drop_ipv4_err / drop_ipv6_err (odp_parse.c:383-387, 392-396): the L4
+	// part is never reached
+	if ((err & E_IP) && (((f & F_IPV4) && (opt & OPT_DROP_V4)) ||
+			     ((f & F_IPV6) && (opt & OPT_DROP_V6)))) {
+		r.l4 = 0xFFFFu;
+		r.flags = f;
+		r.err = err;
+		r.ret = -1;
+		return r;
+	}
+
+	int ret = 0;
+	f |= F_L4;
+	switch (ip_proto) {
+	case 1u:
+	case 58u:
+		f |= F_ICMP;
+		break;
+	case 4u:
+		break;
+	case 6u:
+		f |= F_TCP;
+		if (!non_first) {
+			if (off + 20u > len)
+				ret = -1;
+			else if ((rb(k, off + 12) >> 4) < 5u)
+				err |= E_TCP;
+			if ((err & E_TCP) && (opt & OPT_DROP_TCP))
+				ret = -1;
+		}
+		break;
+	case 17u:
+		f |= F_UDP;
+		if (!non_first) {
+			if (off + 8u > len) {
+				ret = -1;
+			} else {
+				uint32_t ports = r32(k, off);
+				uint32_t ulen = be16(k, off + 4);
+				if (ulen < 8u) {
+					err |= E_UDP;
+					if (opt & OPT_DROP_UDP)
+						ret = -1;
+				} else {
+					// parse_udp, odp_parse.c:298-313
+					if ((opt & OPT_UDP_CK) && !(f & F_IPFRAG) && r16(k, off + 6) == 0u) {
+						f |= F_L4CK_DONE;
+						err |= (f & F_IPV4) ? 0u : E_L4CK;
+						r.udp_zero = 1;
+					}
+					if ((ports >> 16) == 0x9411u /* be16(4500) raw */ && ulen > 4u &&
+					    r32(k, off + 8) != 0u)
+						f |= F_IPSEC;
+				}
+			}
+		}
+		break;
+	case 51u:
+		f |= F_IPSEC | F_AH;
+		break;
+	case 50u:
+		f |= F_IPSEC | F_ESP;
+		break;
+	case 132u:
+		f |= F_SCTP;
+		if (!non_first) {
+			if (off + 12u > len)
+				ret = -1;
+			else if (((len - r.l4) & 0xffffu) < 12u)
+				err |= E_SCTP;
+			if ((err & E_SCTP) && (opt & OPT_DROP_SCTP))
+				ret = -1;
+		}
+		break;
+	case 59u:
+		f |= F_NO_NEXT;
+		break;
+	default:
+		f &= ~F_L4;
+		break;
+	}
+	r.flags = f;
+	r.err = err;
+	r.ret = ret < 0 ? -1 : (err != 0 ? 1 : 0);
+	return r;
+}
+
+// ------------------------------------------------------- pktin checksums
+// CRC-32C (Castagnoli, reflected polynomial 0x82F63B78) byte table, the
+// arithmetic of odp_hash_crc32c (arch/default/odp_hash_crc32.c: table-driven,
+// caller-supplied init, no final inversion).
+struct Crc32cTab {
+	uint32_t v[256];
+	constexpr Crc32cTab() : v()
+	{
+		for (uint32_t i = 0; i < 256; ++i) {
+			uint32_t c = i;
+			for (int b = 0; b < 8; ++b)
+				c = (c & 1u) ? (c >> 1) ^ 0x82F63B78u : (c >> 1);
+			v[i] = c;
+		}
+	}
+};
+static __constant__ Crc32cTab c_crc32c;
+
+__device__ __forceinline__ uint32_t crc32c_u8(uint32_t crc, uint32_t b)
+{
+	return c_crc32c.v[(crc ^ b) & 0xffu] ^ (crc >> 8);
+}
+
+// Sum of the little-endian 32-bit words of frame bytes [from, to) (bytes
+// outside are masked to zero), read from HBM in 16-B pieces that start on
+// frame-relative 16-B boundaries, so no piece reaches past the next 16-B
+// boundary after the frame (the batch contract, mi_cls.h).  `from` is even:
+// every 16-bit word of the one's-complement sum stays in one half of a dword.
+__device__ __forceinline__ uint64_t ck_sum_frame(__amdgpu_buffer_rsrc_t rs, uint32_t boff,
+						  uint32_t from, uint32_t to)
+{
+	uint64_t s = 0;
+	for (uint32_t p = from & ~15u; p < to; p += 16u) {
+		const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, boff + p, 0, 0);
+#pragma unroll
+		for (uint32_t j = 0; j < 4; ++j) {
+			const uint32_t q = p + 4u * j;
+			const uint32_t lo = from > q ? min(from - q, 4u) : 0u;
+			const uint32_t hi = to > q ? min(to - q, 4u) : 0u;
+			const uint32_t mhi = hi >= 4u ? ~0u : ((1u << (8u * hi)) - 1u);
+			const uint32_t mlo = lo >= 4u ? ~0u : ((1u << (8u * lo)) - 1u);
+			s += v[j] & mhi & ~mlo;
+		}
+	}
+	return s;
+}
+
+// _odp_packet_l4_chksum (odp_packet.c:2065-2138) for a parse that returned
+// 0, with the partial sums parse_ipv4 / parse_ipv6 / parse_tcp / parse_udp /
+// parse_sctp prepare (odp_parse.c:146-148, 212-214, 267-275, 298-313,
+// 341-351): UDP / TCP one's-complement sum over the pseudo header and
+// [l4, frame_len), SCTP CRC-32C over [l4, frame_len) with the checksum field
+// taken as zero.  Fragments are skipped.  A failure sets l4_chksum_err and
+// the protocol's error bit, and drops the packet under drop_<proto>_err.
+__device__ __forceinline__ void l4_chksum(const Pkt &k, Parsed &p, uint32_t opt,
+					  __amdgpu_buffer_rsrc_t rs, uint32_t boff)
+{
+	if (p.ret != 0 || (p.flags & F_IPFRAG))
+		return;
+	const uint32_t f = p.flags, len = k.len, l3 = p.l3, l4 = p.l4;
+	const uint32_t kind = ((opt & OPT_UDP_CK) && (f & F_UDP) && !p.udp_zero) ? 1u
+		: (((opt & OPT_TCP_CK) && (f & F_TCP)) ? 2u
+		: (((opt & OPT_SCTP_CK) && (f & F_SCTP)) ? 3u : 0u));
+	if (kind == 0u)
+		return;
+	bool bad;
+	if (kind < 3u) {
+		uint64_t s = 0;
+		if (f & F_IPV4) {
+			s = (uint64_t)r32(k, l3 + 12u) + r32(k, l3 + 16u);
+		} else {
+			for (uint32_t i = 0; i < 8u; ++i)
+				s += r32(k, l3 + 8u + 4u * i);
+		}
+		if (kind == 1u)   // udp->length as stored, IPPROTO_UDP << 8
+			s += r16(k, l4 + 4u) + (17u << 8);
+		else              // odp_cpu_to_be_16(frame_len - l4), IPPROTO_TCP << 8
+			s += (((len - l4) & 0xffu) << 8) + (((len - l4) >> 8) & 0xffu) + (6u << 8);
+		s += ck_sum_frame(rs, boff, l4, len);
+		bad = ck_finalize(s) != 0xffffu;   // ~sum != 0
+	} else {
+		uint32_t crc = 0xffffffffu;
+		for (uint32_t i = 0; i < 8u; ++i)
+			crc = crc32c_u8(crc, rb(k, l4 + i));
+		for (uint32_t i = 0; i < 4u; ++i)
+			crc = crc32c_u8(crc, 0u);
+		for (uint32_t o = l4 + 12u; o < len; ++o)
+			crc = crc32c_u8(crc, rb(k, o));
+		bad = ~crc != r32(k, l4 + 8u);
+	}
+	p.flags |= F_L4CK_DONE;
+	if (bad) {
+		p.err |= E_L4CK | (kind == 1u ? E_UDP : (kind == 2u ? E_TCP : E_SCTP));
+		const uint32_t d = kind == 1u ? OPT_DROP_UDP : (kind == 2u ? OPT_DROP_TCP : OPT_DROP_SCTP);
+		p.ret = (opt & d) ? -1 : 1;
+	}
+}
+
+// Branch-light parse for the common header shapes.  Under _odp_parse_eth's
+// rules the L3 offset is one of 14/18/22/26/30 (DIX or SNAP, plus 0-2 tags),
+// so l3 and every L4 offset reached from it are 2 (mod 4): the parse becomes
+// three batches of independent LDS reads (bytes 0-31, the IP header, the
+// L4 header) combined with selects instead of a branch chain.  Lanes it does
+// not cover -- IPv6 HBH/routing chains, or a field past the staged window --
+// report `slow` and take parse_packet() instead; for every other lane the
+// result is identical to parse_packet's.
+__device__ __forceinline__ uint32_t bsw16(uint32_t v)   // be16 of the low half
+{
+	return ((v & 0xffu) << 8) | ((v >> 8) & 0xffu);
+}
+
+// L4 protocol table (one LDS word per IP protocol number, copied in at block
+// start): the F_L4 / kind flags _odp_packet_parse_common_l3_l4 sets for the
+// protocol (odp_parse.c:395-460) in bits 0..26, and in bits 28..29 the L4
+// header check the protocol takes (1 TCP, 2 UDP, 3 SCTP).  Protocol 255 is
+// "no IP" and 0 a bad IP header: neither sets anything.
+#define L4K_TCP 1u
+#define L4K_UDP 2u
+#define L4K_SCTP 3u
+struct L4Tab {
+	uint32_t v[256];
+	constexpr L4Tab() : v()
+	{
+		v[1] = v[58] = F_L4 | F_ICMP;
+		v[4] = F_L4;
+		v[6] = F_L4 | F_TCP | (L4K_TCP << 28);
+		v[17] = F_L4 | F_UDP | (L4K_UDP << 28);
+		v[51] = F_L4 | F_IPSEC | F_AH;
+		v[50] = F_L4 | F_IPSEC | F_ESP;
+		v[132] = F_L4 | F_SCTP | (L4K_SCTP << 28);
+		v[59] = F_L4 | F_NO_NEXT;
+	}
+};
+static __constant__ L4Tab c_l4tab;
+
+// Branch-light parse of the common frame shapes: DIX or SNAP, 0-2 VLAN tags,
+// IPv4 (any IHL / errors), IPv6 without HBH / routing headers, ARP, every L4.
+// The reference places L3 at 14/18/22/26/30, so every L3 and L4 offset here is
+// 2 (mod 4) and all header words are one alignbyte of two window dwords.
+// Per lane it is written as selects (no data-dependent lane branches); the
+// only branches are wave-uniform ones that skip a header family no lane of
+// the tile has (tags / SNAP, IPv4, IPv6, TCP-UDP-SCTP checks), so a tile of
+// untagged IPv4 frames runs just the IPv4 and its L4 code.  Lanes it cannot
+// finish (IPv6 extension chain, L4 header past the window) set `slow` and are
+// re-parsed by parse_packet.  Results are identical to parse_packet for every
+// lane that does not set `slow`.
+__device__ __forceinline__ Parsed parse_fast(const Pkt &k, const uint32_t *l4tab, bool &slow)
+{
+	Parsed r;
+	const uint32_t len = k.len;
+	const uint32_t w0 = k.w[0], w1 = k.w[RS], w3 = k.w[3 * RS];
+
+	uint32_t f = F_L2 | F_ETH;
+	f |= len > 1514u ? F_JUMBO : 0u;
+	f |= (w0 & 1u) << 8;   // F_ETH_MCAST
+	f |= (w0 == 0xffffffffu && (w1 & 0xffffu) == 0xffffu) ? F_ETH_BCAST : 0u;
+	const uint32_t et0 = bsw16(w3);
+	uint32_t e = et0, off = 14u, err = 0u;
+	bool snap_err = false;
+	if (__ballot(et0 < 1514u || et0 == 0x88A8u || et0 == 0x8100u) != 0ull) {
+		// some lane has SNAP or a tag
+		uint32_t w[8];
+#pragma unroll
+		for (int i = 0; i < 8; ++i) {
+			w[i] = k.w[i * RS];
+			// opaque register value: keeps the selects below v_cndmask
+			// instead of letting the compiler fold them into an indexed
+			// (scratch) load of w[]
+			asm("" : "+v"(w[i]));
+		}
+		const bool snap = et0 < 1514u;
+		snap_err = snap && et0 > len - 14u;
+		e = snap ? bsw16(w[5]) : et0;
+		off = snap ? 22u : 14u;
+		// outer tag: type at off+2 = 16 / 24
+		const bool qinq = e == 0x88A8u;
+		e = qinq ? bsw16(snap ? w[6] : w[4]) : e;
+		off += qinq ? 4u : 0u;
+		// inner tag: type at off+2 = 16 / 20 / 24 / 28 (off = 14 + 8 snap +
+		// 4 qinq); selected by the two booleans, not by an index (an index
+		// would make the compiler spill w[] to scratch)
+		const bool vlan = e == 0x8100u;
+		const uint32_t wv = snap ? (qinq ? w[7] : w[6]) : (qinq ? w[5] : w[4]);
+		e = vlan ? bsw16(wv) : e;
+		off += vlan ? 4u : 0u;
+		err = snap_err ? E_SNAP : 0u;
+		e = snap_err ? 0u : e;
+		off = snap_err ? 14u : off;
+		f |= (!snap_err && qinq) ? (F_QINQ | F_VLAN) : 0u;
+		f |= (!snap_err && vlan) ? F_VLAN : 0u;
+	}
+	const bool short_l2 = !snap_err && off > len;
+	f = short_l2 ? F_L2 : f;
+	e = short_l2 ? 0u : e;
+	const uint32_t l3 = off;
+	r.l3 = l3;
+
+	// IP header bytes l3 .. l3+27 (dwords jb .. jb+7, byte shift 2)
+	const uint32_t jb = (l3 - 2u) >> 2;
+	uint32_t h[8], hb[7];
+#pragma unroll
+	for (int i = 0; i < 8; ++i)
+		h[i] = k.w[(jb + i) * RS];
+#pragma unroll
+	for (int i = 0; i < 7; ++i)
+		hb[i] = __builtin_amdgcn_alignbyte(h[i + 1], h[i], 2u);   // bytes l3+4i .. +3
+
+	const bool is4 = e == 0x0800u, is6 = e == 0x86DDu, isarp = e == 0x0806u;
+	f |= (is4 || is6 || isarp) ? F_L3 : 0u;
+	f |= isarp ? F_ARP : 0u;
+	uint32_t ip_proto = (is4 || is6) ? 0u : 255u;   // bad IP header / no IP
+	uint32_t l4 = 0xFFFFu;
+	bool non_first = false, sl = false;
+	if (__ballot(is4) != 0ull) {
+		// IPv4 (parse_ipv4, odp_parse.c:112-167)
+		const uint32_t vi = hb[0] & 0xffu, ihl = vi & 0xfu;
+		const uint32_t tot = bsw16(hb[0] >> 16);
+		const bool bad4 = ihl < 5u || (vi >> 4) != 4u || 20u > len - l3 || tot > len - l3;
+		const uint32_t frag = bsw16(hb[1] >> 16);
+		const uint32_t dst = __builtin_bswap32(hb[4]);
+		uint32_t f4 = F_IPV4;
+		f4 |= ihl > 5u ? F_IPOPT : 0u;
+		f4 |= (frag & 0x3fffu) ? F_IPFRAG : 0u;
+		f4 |= dst == 0xffffffffu ? F_IP_BCAST : 0u;
+		f4 |= (dst >> 28) == 0xeu ? F_IP_MCAST : 0u;
+		const bool ok4 = is4 && !bad4;
+		f |= is4 ? (bad4 ? F_IPV4 : f4) : 0u;
+		err |= (is4 && bad4) ? E_IP : 0u;
+		ip_proto = ok4 ? ((hb[2] >> 8) & 0xffu) : ip_proto;
+		l4 = ok4 ? l3 + ihl * 4u : l4;
+		non_first = ok4 && (frag & 0x1fffu) != 0u;
+	}
+	if (__ballot(is6) != 0ull) {
+		// IPv6 (parse_ipv6, :174-246)
+		const uint32_t plen = bsw16(hb[1]);
+		const bool bad6 = ((hb[0] & 0xffu) >> 4) != 6u || 40u > len - l3 || plen + 40u > len - l3;
+		const uint32_t nh = (hb[1] >> 16) & 0xffu;
+		uint32_t f6 = F_IPV6;
+		f6 |= (hb[6] & 0xffu) == 0xffu ? F_IP_MCAST : 0u;
+		f6 |= nh == 44u ? (F_IPOPT | F_IPFRAG) : 0u;
+		const bool ok6 = is6 && !bad6;
+		f |= is6 ? (bad6 ? F_IPV6 : f6) : 0u;
+		err |= (is6 && bad6) ? E_IP : 0u;
+		ip_proto = ok6 ? nh : ip_proto;
+		l4 = ok6 ? l3 + 40u : l4;
+		sl = ok6 && (nh == 0u || nh == 43u);   // extension chain: general parser
+	}
+
+	// L4 (_odp_packet_parse_common_l3_l4, :395-460)
+	const uint32_t pt = l4tab[ip_proto];
+	f |= pt & 0x0fffffffu;
+	const uint32_t kc = pt >> 28;
+	const bool chk = kc != 0u && !non_first;   // a TCP / UDP / SCTP header to check
+	bool drop = false;
+	if (__ballot(chk) != 0ull) {
+		// L4 header bytes l4 .. l4+15 (dwords jl .. jl+4, byte shift 2)
+		const uint32_t jl = min((l4 - 2u) >> 2, (uint32_t)(WIN / 4 - 4));
+		uint32_t m[5], lb[4];
+#pragma unroll
+		for (int i = 0; i < 5; ++i)
+			m[i] = k.w[(jl + i) * RS];
+#pragma unroll
+		for (int i = 0; i < 4; ++i)
+			lb[i] = __builtin_amdgcn_alignbyte(m[i + 1], m[i], 2u);
+		const bool tcp = chk && kc == L4K_TCP, udp = chk && kc == L4K_UDP;
+		const bool sctp = chk && kc == L4K_SCTP;
+		// bytes the checks below use: TCP data offset (l4+12), UDP ports and
+		// length (l4..l4+5) and, for destination port 4500, the NAT-T marker
+		// (l4+8..l4+11); a lane whose bytes are not all staged takes the
+		// general parser (the unused bytes of m[] may lie past the window)
+		const uint32_t l4need = tcp ? 13u : (udp ? (((lb[0] >> 16) == 0x9411u) ? 12u : 6u) : 0u);
+		sl = sl || (chk && l4 + l4need > k.win);
+		// TCP (parse_tcp, :299-316)
+		const bool tcp_drop = tcp && l4 + 20u > len;
+		err |= (tcp && !tcp_drop && ((lb[3] & 0xffu) >> 4) < 5u) ? E_TCP : 0u;
+		// UDP (parse_udp, :321-354)
+		const bool udp_drop = udp && l4 + 8u > len;
+		const uint32_t ulen = bsw16(lb[1]);
+		const bool udp_ok = udp && !udp_drop;
+		err |= (udp_ok && ulen < 8u) ? E_UDP : 0u;
+		f |= (udp_ok && ulen >= 8u && (lb[0] >> 16) == 0x9411u && ulen > 4u && lb[2] != 0u)
+			? F_IPSEC : 0u;
+		// SCTP (parse_sctp, :362-388)
+		const bool sctp_drop = sctp && l4 + 12u > len;
+		err |= (sctp && !sctp_drop && ((len - l4) & 0xffffu) < 12u) ? E_SCTP : 0u;
+		drop = tcp_drop || udp_drop || sctp_drop;
+	}
+
+	slow = sl;
+	r.l4 = l4;
+	r.flags = f;
+	r.err = err;
+	r.ret = drop ? -1 : (err != 0u ? 1 : 0);
+	return r;
+}
+
+// --------------------------------------------------------- field registers
+// What the term verifiers compare is read on use from the packet window
+// (LDS; HBM past it) rather than cached in registers: the window stays valid
+// for the whole tile, and caching every kind the program might use would
+// hold ~20 VGPRs through the descent.
+struct Fields {
+	Pkt k;
+	uint32_t l3, l4, f;
+};
+
+// Where the key words of a term kind sit (verify_pmr_<term>,
+// odp_classification.c:931-1357): 4-byte little-endian words at
+// base + add, or base + alt when the lane's flags have `altf`
+// (QinQ outer tag, IPv4 vs IPv6 next-header, AH vs ESP SPI); base is the
+// frame start, L3 or L4.  The term's mask words cut each word down to the
+// field (e.g. 0xffff for a 16-bit field), so every kind but LEN, PCP and
+// DSCP is "read words, AND mask".  gate: the packet has the field iff its
+// flags share a bit with `gate` (~0: always).  The verifiers' presence tests
+// map onto single flag masks: eth && vlan is F_VLAN (both parsers set VLAN
+// only on frames that keep F_ETH), vlan || qinq, ipv4 || ipv6, ah || esp;
+// "l2 && l3 valid" (custom L3) is F_L2 plus the l3 != invalid test in
+// field_off.
+enum { FB_FRAME = 0, FB_L3 = 1, FB_L4 = 2 };
+// classification-block pseudo kind: UDP and TCP port terms with one mask
+// (class_of), the raw port word at l4 tagged with the protocol
+#define K_L4PORT 0x40u
+struct FDesc {
+	uint32_t base, add, alt, altf, gate;
+};
+
+__host__ __device__ inline FDesc fdesc(uint32_t kind, uint32_t toff)
+{
+	FDesc d = { FB_FRAME, 0u, 0u, 0u, 0u };
+	switch (kind) {
+	case MI_K_ETH0: d = { FB_FRAME, 12u, 12u, 0u, F_ETH }; break;
+	case MI_K_ETHX: d = { FB_FRAME, 16u, 20u, F_QINQ, F_VLAN | F_QINQ }; break;
+	case MI_K_VID0: d = { FB_FRAME, 14u, 14u, 0u, F_VLAN }; break;
+	case MI_K_VIDX: d = { FB_FRAME, 14u, 18u, F_QINQ, F_VLAN | F_QINQ }; break;
+	case MI_K_DMAC: d = { FB_FRAME, 0u, 0u, 0u, F_ETH }; break;
+	case MI_K_PROTO: d = { FB_L3, 6u, 9u, F_IPV4, F_IPV4 | F_IPV6 }; break;
+	case MI_K_UDP_DPORT:
+	case MI_K_UDP_SPORT: d = { FB_L4, 0u, 0u, 0u, F_UDP }; break;
+	case MI_K_TCP_DPORT:
+	case MI_K_TCP_SPORT: d = { FB_L4, 0u, 0u, 0u, F_TCP }; break;
+	case K_L4PORT: d = { FB_L4, 0u, 0u, 0u, F_UDP | F_TCP }; break;
+	case MI_K_SIP: d = { FB_L3, 12u, 12u, 0u, F_IPV4 }; break;
+	case MI_K_DIP: d = { FB_L3, 16u, 16u, 0u, F_IPV4 }; break;
+	case MI_K_SIP6: d = { FB_L3, 8u, 8u, 0u, F_IPV6 }; break;
+	case MI_K_DIP6: d = { FB_L3, 24u, 24u, 0u, F_IPV6 }; break;
+	case MI_K_SPI: d = { FB_L4, 0u, 4u, F_AH, F_AH | F_ESP }; break;
+	case MI_K_CUSTOM_FRAME: d = { FB_FRAME, toff, toff, 0u, ~0u }; break;
+	case MI_K_CUSTOM_L3: d = { FB_L3, toff, toff, 0u, F_L2 }; break;
+	default: break;
+	}
+	return d;
+}
+
+__device__ __forceinline__ bool kind_special(uint32_t kind)
+{
+	return kind == MI_K_LEN || kind == MI_K_PCP0 || kind == MI_K_DSCP || kind == MI_K_NEVER ||
+	       kind == MI_K_ALWAYS;
+}
+
+// LEN / PCP / DSCP values and presence (NEVER: absent, ALWAYS: present)
+__device__ __forceinline__ bool special_value(uint32_t kind, const Fields &x, uint32_t &v)
+{
+	if (kind == MI_K_LEN) {
+		v = x.k.len;
+		return true;
+	}
+	if (kind == MI_K_PCP0) {
+		v = (r16(x.k, 14) & 0xffu) >> 5;
+		return (x.f & F_VLAN) != 0u;
+	}
+	if (kind == MI_K_DSCP) {
+		v = (x.f & F_IPV4) ? (rb(x.k, x.l3 + 1) >> 2)
+				   : ((be32(x.k, x.l3) & 0x0fc00000u) >> 22);
+		return (x.f & (F_IPV4 | F_IPV6)) != 0u;
+	}
+	v = 0;
+	return kind == MI_K_ALWAYS;
+}
+
+// Byte offset of a kind's first key word in the lane's frame, and whether the
+// packet has the field (custom kinds: the frame must extend past
+// offset + size, verify_pmr_custom_*).
+__device__ __forceinline__ uint32_t field_off(const FDesc &d, uint32_t kind, uint32_t size,
+					      const Fields &x, bool &present)
+{
+	const uint32_t base = d.base == FB_L3 ? x.l3 : (d.base == FB_L4 ? x.l4 : 0u);
+	const uint32_t o = base + ((x.f & d.altf) ? d.alt : d.add);
+	present = d.gate == ~0u || (x.f & d.gate) != 0u;
+	if (kind == MI_K_CUSTOM_L3)
+		present = present && x.l3 != 0xFFFFu;
+	if (kind == MI_K_CUSTOM_FRAME || kind == MI_K_CUSTOM_L3)
+		present = present && !(x.k.len <= o + size);
+	return o;
+}
+
+__device__ __forceinline__ Fields fields_of(const Pkt &k, const Parsed &p)
+{
+	Fields x;
+	x.k = k;
+	x.l3 = p.l3;
+	x.l4 = p.l4;
+	x.f = p.flags;
+	return x;
+}
+
+// ----------------------------------------------------------- Toeplitz hash
+// thash_softrss (protocols/thash.h:82-99) with the default 40-B key
+// (odp_classification.c:50-58), key words in big-endian order.
+static __constant__ uint32_t c_rss_key[10] = {
+	0x6d5a56dau, 0x255b0ec2u, 0x4167253du, 0x43a38fb0u, 0xd0ca2bcbu,
+	0xae7b30b4u, 0x77cb2da3u, 0x8030f20cu, 0x6a42b73bu, 0xbeac01fau,
+};
+
+__device__ __forceinline__ uint32_t thash_word(uint32_t w, uint32_t j)
+{
+	uint32_t kj = c_rss_key[j], kn = c_rss_key[j + 1], h = 0;
+	while (w) {
+		uint32_t p = 31u - __builtin_clz(w);   // bit position from LSB
+		uint32_t i = 31u - p;                  // reference loop index
+		h ^= (kj << i) | (i ? (kn >> (32u - i)) : 0u);
+		w &= ~(1u << p);
+	}
+	return h;
+}
+
+// packet_rss_hash, odp_classification.c:1773-1839
+__device__ __forceinline__ uint32_t rss_hash(const Pkt &k, const Parsed &p, uint32_t hp)
+{
+	const uint32_t f = p.flags;
+	uint32_t h = 0, j = 0;
+	bool l4 = ((f & F_TCP) && (hp & 8u)) || ((f & F_UDP) && (hp & 4u));
+	if (f & F_IPV4) {
+		if (hp & 1u) {
+			h ^= thash_word(r32(k, p.l3 + 12), 0);
+			h ^= thash_word(r32(k, p.l3 + 16), 1);
+			j = 2;
+		}
+		if (l4) {
+			// without L3 hashing the reference hashes an uninitialised word 0;
+			// here word 0 is taken as zero (undefined in the reference)
+			if (j == 2)
+				h ^= thash_word(r32(k, p.l4), 2);
+		}
+	} else if (f & F_IPV6) {
+		if (hp & 2u) {
+#pragma unroll
+			for (uint32_t i = 0; i < 4; ++i) {
+				h ^= thash_word(be32(k, p.l3 + 8 + 4 * i), i);
+				h ^= thash_word(be32(k, p.l3 + 24 + 4 * i), 4 + i);
+			}
+			j = 8;
+		}
+		if (l4 && j == 8)
+			h ^= thash_word(r32(k, p.l4), 8);
+	}
+	return h;
+}
+
+// ------------------------------------------------------ device rule program
+// mi_cls_rules_load() assembles the mi_cls.h table into this private,
+// read-only encoding (32-bit words):
+//
+//   [0, 16)              header (DH_* below)
+//   [hot_off, +hot_words)  HOT region -- everything a lane may look up with its
+//                        own (per-lane) index.  All offsets inside it are
+//                        relative to hot_off, so the kernel can read it from
+//                        HBM or from a copy in LDS with the same indices:
+//      CoS table        4 words per CoS slot: #rules, bit-vector block (0 =
+//                       linear scan), meta = action | num_queue<<8 |
+//                       hash_proto<<16 | index<<24, first rule record
+//      BV blocks        see below
+//   [prog_off, ...)      COLD region -- 16-word rule records, read only with
+//                        wave-uniform (scalar) loads by the linear engine:
+//        w0  = inline terms | ext terms<<8 | mark<<16
+//        w1  = dst CoS | ext word offset<<8
+//        w2.. terms: op word (kind | size<<8 | nw<<16), [offset word for custom
+//             kinds], then nw (mask, value) word pairs; terms that do not fit
+//             the 14 inline words continue at the ext offset.
+typedef const __attribute__((address_space(4))) uint32_t *cword_t;   // scalar loads
+typedef const __attribute__((address_space(3))) uint32_t *lword_t;   // LDS
+typedef const __attribute__((address_space(1))) uint32_t *gword_t;   // HBM
+
+enum { DH_MAGIC = 0, DH_NCOS, DH_DEFAULT, DH_ERROR, DH_DEFAULT_VALID, DH_USED, DH_MAX_HOPS,
+       DH_HOT_OFF, DH_PROG_OFF, DH_TOTAL, DH_HOT_WORDS,
+       // furthest byte past L3 / L4 / the frame start any term (or the hash
+       // queue tuple) of the program reads: the kernel's window predictor
+       DH_L3END, DH_L4END, DH_FREND, DH_WORDS = 16 };
+#define DEV_MAGIC 0x33564544u   // "DEV3"
+#define REC_WORDS 16u
+#define COS_WORDS 4u
+#define C_NR 0u
+#define C_BV 1u
+#define C_META 2u
+#define C_REC0 3u
+#define BV_MAX_CLS 8u
+#define BV_CLS_WORDS 16u
+#define BV_WIDE_WORDS 8u        // wide bitmap rows: up to 256 rules
+// class words 14-15: the field descriptor of the class's kind (fdesc()),
+// resolved at rule load so the device decodes it instead of switching on
+// kind: w14 = add | alt << 16; w15 = gate (flag mask, bits 0-23) | base << 24
+// | alt-flag code << 26 (1 QinQ, 2 IPv4, 3 AH) | BVF_* << 28
+#define BVC_AO 14u
+#define BVC_DESC 15u
+#define BVF_SPECIAL 1u          // LEN / PCP / DSCP: special_value()
+#define BVF_CUSTOM 2u           // custom frame / L3: length test
+#define BVF_L3 4u               // custom L3: l3 must be valid
+#define BVF_TAG 8u              // merged UDP/TCP port class: protocol tag at bit cr(3)
+#define BV_EMPTY 0xFFFFFFFFu
+#define BV_NONE 0xFFFFFFFEu
+
+// Classification block of a CoS ("BV" block for historical reasons), used
+// when its rules fall into at most BV_MAX_CLS key classes (a key class is one
+// (term kind, mask[, offset, size]) combination).  build_bv() explains the
+// modes; the layout (word indices into the hot region) is:
+//   b[0] mode (0 direct, 1 candidate, 2 bitmap, 3 wide bitmap), b[1] #classes,
+//   b[2] result words (dst | leaf<<8 | mark<<16 per rule; leaf = the
+//   destination CoS has no rules, so the descent ends there), b[3] first rule
+//   without a classified term (BV_NONE: none), b[4] rule records (bitmap:
+//   alive row; wide: block-relative index of the nw-word alive row), b[5]
+//   record words, b[6] wide: nw = words per row
+//   b[8 + 16 k ...] class k: kind, nkey, miss value (direct: first rule,
+//                   bitmap: row, wide: index of the miss row), offset, size,
+//                   mask[4], #slots, table offset, cuckoo multipliers m1, m2,
+//                   list base
+//   table slot (nkey + 1 words): key words, value (0: empty)
+//     direct: 1 + first live rule with this key or without a term of the
+//             class (BV_EMPTY: none)
+//     bitmap: the 32-bit row of rules with this key or without a term
+//     wide:   index of the nw-word row of rules with this key or without a
+//             term of the class (rows are deduplicated)
+//     candidate: key id | list length << 12 | list offset << 20; the list
+//             holds the rules filed under this key, in scan order
+//   rule record (candidate, 1 + ceil(#classes / 2) words): constrained-
+//             class mask (bit 31: never holds), then the required key id of
+//             class c in half c & 1 of word 1 + c / 2
+
+__device__ __forceinline__ bool eq1(uint32_t x, uint32_t m, uint32_t v)
+{
+	return (x & m) == v;
+}
+
+// verify_pmr_<term> for one term whose words start at prog[q] (uniform);
+// returns the lane's verdict and advances q past the term.
+__device__ __forceinline__ bool term_ok(cword_t prog, uint32_t &q, const Pkt &k, const Parsed &p,
+					const Fields &x)
+{
+	const uint32_t op = prog[q];
+	const uint32_t kind = op & 0xffu;
+	const uint32_t sz = (op >> 8) & 0xffu;
+	const uint32_t nw = (op >> 16) & 0xffu;
+	if (kind_special(kind)) {
+		uint32_t v;
+		const bool ok = special_value(kind, x, v) &&
+				(kind == MI_K_ALWAYS || eq1(v, prog[q + 1], prog[q + 2]));
+		q += 1u + 2u * nw;
+		return ok;
+	}
+	const bool custom = kind == MI_K_CUSTOM_FRAME || kind == MI_K_CUSTOM_L3;
+	const FDesc d = fdesc(kind, custom ? prog[q + 1] : 0u);
+	const uint32_t q0 = q + (custom ? 2u : 1u);
+	bool ok;
+	const uint32_t o = field_off(d, kind, sz, x, ok);
+	for (uint32_t i = 0; i < nw; ++i)
+		ok = ok && eq1(r32(k, o + 4u * i), prog[q0 + 2u * i], prog[q0 + 2u * i + 1u]);
+	q = q0 + 2u * nw;
+	return ok;
+}
+
+__device__ __forceinline__ uint32_t bv_fold(const uint32_t k[4])
+{
+	uint32_t h = k[0] * 0x9E3779B1u ^ k[1] * 0x85EBCA77u ^ k[2] * 0xC2B2AE3Du ^ k[3] * 0x27D4EB2Fu;
+	return h ^ (h >> 15);
+}
+
+// Cuckoo bucket of a key: x = the key word (one-word keys) or bv_fold (longer
+// keys), folded to 24 bits that depend on every key bit, times a 24-bit
+// multiplier; the top 16 bits of the low product word, scaled to [0, nb)
+// (nb <= 65536).  Two v_mul_u32_u24 (full rate, unlike a 32-bit multiply).
+// host_bucket() is the same arithmetic.
+__device__ __forceinline__ uint32_t bv_bucket(uint32_t x, uint32_t m, uint32_t nb)
+{
+	// (__umul24 returns int: shift the unsigned products)
+	const uint32_t h = (uint32_t)__umul24(x ^ (x >> 16), m);
+	return (uint32_t)__umul24(h >> 16, nb) >> 16;
+}
+
+// Word readers of a classification block: wave-uniform blocks are read with
+// scalar loads from HBM (DescU), per-lane blocks from the hot region (LDS or
+// HBM, DescL).
+struct DescU {
+	cword_t p;
+	__device__ __forceinline__ uint32_t operator()(uint32_t i) const { return p[i]; }
+	__device__ __forceinline__ DescU at(uint32_t o) const { return DescU{ p + o }; }
+};
+template <typename T> struct DescL {
+	T p;
+	uint32_t b;
+	__device__ __forceinline__ uint32_t operator()(uint32_t i) const { return p[b + i]; }
+	__device__ __forceinline__ DescL at(uint32_t o) const { return DescL{ p, b + o }; }
+};
+
+// Key of a packet for one class: the masked field the class's terms
+// compare, and whether the packet has that field at all (the term's gate).
+template <typename D>
+__device__ __forceinline__ bool bv_key(const D &cr, const Pkt &k, const Parsed &p, const Fields &x,
+				       uint32_t key[4])
+{
+	const uint32_t nk = cr(1), desc = cr(BVC_DESC), dfl = desc >> 28;
+	key[0] = key[1] = key[2] = key[3] = 0;
+	if (dfl & BVF_SPECIAL) {
+		uint32_t v;
+		const bool pr = special_value(cr(0), x, v);
+		key[0] = v & cr(5);
+		return pr;
+	}
+	// the class's field descriptor (fdesc() of its kind, resolved at load)
+	const uint32_t ao = cr(BVC_AO), fb = (desc >> 24) & 3u, ac = (desc >> 26) & 3u;
+	const uint32_t altf = ac == 1u ? F_QINQ : (ac == 2u ? F_IPV4 : (ac == 3u ? F_AH : 0u));
+	const uint32_t base = fb == FB_L3 ? x.l3 : (fb == FB_L4 ? x.l4 : 0u);
+	const uint32_t o = base + ((x.f & altf) ? (ao >> 16) : (ao & 0xffffu));
+	bool present = (x.f & desc & 0xffffffu) != 0u;
+	if (dfl & BVF_CUSTOM)   // verify_pmr_custom_*: the frame extends past the field
+		present = present && ((dfl & BVF_L3) == 0u || x.l3 != 0xFFFFu) &&
+			  !(x.k.len <= o + cr(4));
+	key[0] = r32(k, o) & cr(5);
+	if (dfl & BVF_TAG)   // merged UDP/TCP port class
+		key[0] |= ((x.f & F_UDP) ? 1u : 2u) << cr(3);
+	if (nk > 1u) {
+		key[1] = r32(k, o + 4u) & cr(6);
+		if (nk > 2u) {
+			key[2] = r32(k, o + 8u) & cr(7);
+			key[3] = r32(k, o + 12u) & cr(8);
+		}
+	}
+	return present;
+}
+
+// 16-byte read of the hot region (LDS: ds_read_b128, HBM: global dwordx4);
+// i is a multiple of 4 (hot-region blocks, buckets and rows are 16-B aligned)
+__device__ __forceinline__ u32x4 ld4(lword_t H, uint32_t i)
+{
+	return *(const __attribute__((address_space(3))) u32x4 *)(H + i);
+}
+__device__ __forceinline__ u32x4 ld4(gword_t H, uint32_t i)
+{
+	return *(const __attribute__((address_space(1))) u32x4 *)(H + i);
+}
+
+// Two-choice cuckoo lookup (both candidate buckets read at once, no probe
+// loop).  One-word keys: buckets of two (key, value) slots, 16 B, read with
+// one 16-B load each.  Longer keys: one slot of nk key words + value per
+// bucket.  An empty slot has key words 0 and value 0, and a key sits in at
+// most one slot, so OR-ing the values of the slots whose key words equal the
+// packet's gives the hit's value, or 0 on a miss.
+template <typename D, typename T>
+__device__ __forceinline__ uint32_t bv_lookup(const D &cr, T H, const uint32_t key[4], bool act)
+{
+	// ns = bucket count
+	const uint32_t nk = cr(1), ns = cr(9), tbl = cr(10), m1 = cr(11), m2 = cr(12);
+	uint32_t val = 0;
+	if (nk == 1u) {
+		// one-word keys (the common case): bv_fold with zero upper words
+		const u32x4 b1 = ld4(H, tbl + 4u * bv_bucket(key[0], m1, ns));
+		const u32x4 b2 = ld4(H, tbl + 4u * bv_bucket(key[0], m2, ns));
+		val = (b1[0] == key[0] ? b1[1] : 0u) | (b1[2] == key[0] ? b1[3] : 0u) |
+		      (b2[0] == key[0] ? b2[1] : 0u) | (b2[2] == key[0] ? b2[3] : 0u);
+		return act ? val : 0u;
+	}
+	const uint32_t f = bv_fold(key);
+	const uint32_t sw = nk + 1u;
+#pragma unroll
+	for (uint32_t s = 0; s < 2; ++s) {
+		const uint32_t a = tbl + bv_bucket(f, s ? m2 : m1, ns) * sw;
+		bool e = H[a] == key[0] && H[a + 1] == key[1];
+		if (nk > 2)
+			e = e && H[a + 2] == key[2] && H[a + 3] == key[3];
+		const uint32_t v = H[a + nk];
+		val = (act && e && v != 0u) ? v : val;
+	}
+	return val;
+}
+
+// Classification block evaluation of one CoS for the lanes in `act`
+// (see build_bv for the two modes).  `blk` reads the CoS's block (wave-
+// uniform or per lane); H is the hot region the block's offsets index.  On
+// return, lanes of `act` with a matching rule have hit = 1 and the rule's
+// destination CoS / mark / leaf bit in nxt / nmark / nleaf.
+template <typename D, typename T>
+__device__ __forceinline__ void bv_eval(const D &blk, T H, bool act, const Pkt &k, const Parsed &p,
+					const Fields &x, uint32_t &hit, uint32_t &nxt, uint32_t &nmark,
+					uint32_t &nleaf)
+{
+	const uint32_t mode = blk(0), ncls = blk(1), res = blk(2);
+	uint32_t first = BV_NONE;
+	if (mode == 0u) {
+		// direct: one class, the slot holds 1 + the first live rule of its
+		// key (BV_EMPTY: none); a miss takes the block's "no term" rule
+		const D cr = blk.at(8u);
+		uint32_t key[4];
+		const bool present = bv_key(cr, k, p, x, key);
+		const uint32_t val = bv_lookup(cr, H, key, act && present);
+		first = val != 0u ? (val == BV_EMPTY ? BV_NONE : val - 1u) : cr(2);
+	} else if (mode == 2u) {
+		// bitmap: AND of the classes' 32-bit rows and the alive row
+		uint32_t acc = blk(4);
+#pragma unroll
+		for (uint32_t kc = 0; kc < BV_MAX_CLS; ++kc) {
+			if (kc < ncls) {
+				const D cr = blk.at(8u + BV_CLS_WORDS * kc);
+				uint32_t key[4];
+				const bool present = bv_key(cr, k, p, x, key);
+				const uint32_t val = bv_lookup(cr, H, key, act && present);
+				acc &= val != 0u ? val : cr(2);
+			}
+		}
+		first = acc != 0u ? (uint32_t)__builtin_ctz(acc) : BV_NONE;
+	} else if (mode == 3u) {
+		// wide bitmap (33..256 rules): AND of the classes' rows (in the hot
+		// region, BV_WIDE_WORDS words each, zero past the rule count; a miss
+		// takes the class's miss row) and the alive row; the lowest set bit
+		// is the first holding rule
+		// rows are split in halves: words 0-3 at the value, words 4-7
+		// `half` words further (consecutive rows are then 16 B apart, so the
+		// 16-lane groups of a 16-B LDS read spread over all 64 banks)
+		const uint32_t ar = blk(4), half = blk(7);
+		uint32_t acc[BV_WIDE_WORDS];
+#pragma unroll
+		for (uint32_t i = 0; i < BV_WIDE_WORDS; ++i)
+			acc[i] = blk(ar + i);
+#pragma unroll
+		for (uint32_t kc = 0; kc < BV_MAX_CLS; ++kc) {
+			if (kc < ncls) {
+				const D cr = blk.at(8u + BV_CLS_WORDS * kc);
+				uint32_t key[4];
+				const bool present = bv_key(cr, k, p, x, key);
+				const uint32_t val = bv_lookup(cr, H, key, act && present);
+				const uint32_t ro = val != 0u ? val : cr(2);
+				const u32x4 r0 = ld4(H, ro), r1 = ld4(H, ro + half);
+#pragma unroll
+				for (uint32_t i = 0; i < 4; ++i) {
+					acc[i] &= r0[i];
+					acc[4 + i] &= r1[i];
+				}
+			}
+		}
+#pragma unroll
+		for (int i = (int)BV_WIDE_WORDS - 1; i >= 0; --i)
+			first = acc[i] != 0u ? 32u * (uint32_t)i + (uint32_t)__builtin_ctz(acc[i]) : first;
+	} else {
+		// candidate: key id per class, then the candidates' records
+		const uint32_t rec0 = blk(4), rw = blk(5);
+		uint32_t v[BV_MAX_CLS], lb[BV_MAX_CLS];
+#pragma unroll
+		for (uint32_t kc = 0; kc < BV_MAX_CLS; ++kc) {
+			v[kc] = 0u;
+			lb[kc] = 0u;
+			if (kc < ncls) {
+				const D cr = blk.at(8u + BV_CLS_WORDS * kc);
+				uint32_t key[4];
+				const bool present = bv_key(cr, k, p, x, key);
+				v[kc] = bv_lookup(cr, H, key, act && present);
+				lb[kc] = cr(13);
+			}
+		}
+		first = blk(3);   // the first rule without a classified term
+#pragma unroll
+		for (uint32_t kc = 0; kc < BV_MAX_CLS; ++kc) {
+			if (kc < ncls) {
+				// value = key id | list length << 12 | list offset << 20
+				uint32_t j = 0, n = (v[kc] >> 12) & 0xffu;
+				const uint32_t lo = lb[kc] + (v[kc] >> 20);
+				for (;;) {
+					const bool more = act && j < n;
+					if (__ballot(more) == 0ull)
+						break;
+					if (more) {
+						const uint32_t r = H[lo + j];
+						bool ok = r < first;
+						if (ok) {
+							const uint32_t rec = rec0 + r * rw;
+							const uint32_t m = H[rec];
+							ok = (m >> 31) == 0u;
+#pragma unroll
+							for (uint32_t c = 0; c < BV_MAX_CLS; c += 2) {
+								if (c < ncls && ((m >> c) & 3u)) {
+									const uint32_t w = H[rec + 1u + (c >> 1)];
+									ok = ok && (!((m >> c) & 1u) ||
+										    (v[c] & 0xfffu) == (w & 0xffffu));
+									ok = ok && (!((m >> (c + 1)) & 1u) ||
+										    (v[c + 1] & 0xfffu) == (w >> 16));
+								}
+							}
+						}
+						first = ok ? r : first;
+						// lists are in scan order: the first candidate that
+						// holds, or reaches `first`, ends this list
+						n = (ok || r >= first) ? 0u : n;
+						++j;
+					}
+				}
+			}
+		}
+	}
+	const bool h = act && first != BV_NONE;
+	const uint32_t rw2 = H[res + (h ? first : 0u)];
+	nxt = h ? (rw2 & 0xffu) : nxt;
+	nleaf = h ? ((rw2 >> 8) & 1u) : nleaf;
+	nmark = h ? (rw2 >> 16) : nmark;
+	hit = h ? 1u : hit;
+}
+
+// Linear scan of one wave-uniform CoS's rule records for the lanes in
+// `grp` (verify_pmr over cos->pmr[] in order, first match wins).
+__device__ __forceinline__ void linear_scan(cword_t prog, uint32_t rec0, uint32_t nr, bool grp,
+					    const Pkt &k, const Parsed &p, const Fields &x,
+					    uint32_t &done, uint32_t &nxt, uint32_t &nmark)
+{
+	for (uint32_t r = 0; r < nr; ++r) {
+		const bool cand = grp && done == 0u;
+		if (__ballot(cand) == 0ull)
+			break;
+		const uint32_t base = (rec0 + r) * REC_WORDS;
+		const uint32_t w0 = prog[base];
+		const uint32_t w1 = prog[base + 1];
+		const uint32_t n_in = w0 & 0xfu, n_ext = (w0 >> 8) & 0xfu;
+		// AND of the terms; stop as soon as no lane can still match
+		bool ok = cand;
+		uint32_t q = base + 2;
+		for (uint32_t t = 0; t < n_in; ++t) {
+			if (__ballot(ok) == 0ull)
+				break;
+			ok = term_ok(prog, q, k, p, x) && ok;
+		}
+		if (n_ext && __ballot(ok) != 0ull) {
+			q = w1 >> 8;
+			for (uint32_t t = 0; t < n_ext; ++t) {
+				if (__ballot(ok) == 0ull)
+					break;
+				ok = term_ok(prog, q, k, p, x) && ok;
+			}
+		}
+		nxt = ok ? (w1 & 0xffu) : nxt;
+		nmark = ok ? (w0 >> 16) : nmark;
+		done = ok ? 1u : done;
+	}
+}
+// Diagnostic build only (-DDIAG_STAMPS): per-phase cycle sums per wave,
+// written to a debug buffer nobody else reads (cdna_hip_programming.md §7).
+#ifdef DIAG_STAMPS
+#define NSTAMP 8
+#define STAMP(i)                                                                   \
+	do {                                                                       \
+		__builtin_amdgcn_sched_barrier(0);                                 \
+		unsigned long long t_;                                             \
+		asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_) :: "memory"); \
+		__builtin_amdgcn_sched_barrier(0);                                 \
+		st_acc[i] += t_ - st_last;                                         \
+		st_last = t_;                                                      \
+	} while (0)
+#else
+#define STAMP(i) do { } while (0)
+#endif
+
+// ------------------------------------------------------------------ kernel
+struct KArgs {
+	const uint8_t *pkts;
+	const uint32_t *off;
+	const uint16_t *len;
+	uint32_t n;
+	const uint32_t *dev;         // device rule program (constant address space)
+	mi_cls_result_t *out;
+	unsigned long long *stats;   // MAX_STATS_COS counters, or NULL
+	unsigned long long *diag;    // DIAG_STAMPS builds only
+	uint32_t stats_mask[8];
+	uint32_t opt;                // pktin options (OPT_*), 0: none
+	// window hint across launches of a context: a wave of block 0 whose
+	// frames needed bytes 64.. stores this launch's sequence number `seq` in
+	// *hint; the next launch (seq + 1) starts its predictor from it.  Only a
+	// performance hint -- results never depend on it.
+	uint32_t *hint;
+	uint32_t seq;
+};
+
+__device__ __forceinline__ bool stats_bit(const KArgs &a, uint32_t c)
+{
+	return c < MAX_STATS_COS && ((a.stats_mask[c >> 5] >> (c & 31u)) & 1u);
+}
+
+// Buffer offset no frame byte reaches: num_records of the packet resource, so
+// a load at or past it returns zeros (batches are < 4 GiB: u32 offsets).
+#define OOB_OFF 0xFFFFFE00u
+
+static_assert(NPIECE == 8 || NPIECE == 6, "WIN must be 96 or 128");
+#define NB (NPIECE - 4)         // upper pieces (phase B)
+
+// Issue the loads of a tile's header windows (64 packets, per-lane
+// descriptors off/len).  The lanes cooperate so that each load instruction
+// covers whole packets' headers: in phase A lane l loads piece l&3 (bytes
+// 16(l&3) ..) of packet 16r + (l>>2), r = 0..3 -- for back-to-back frames an
+// instruction reads 16 x 64 contiguous bytes instead of 64 scattered pieces,
+// a quarter of the cache-line lookups.  Phase B (pieces 4..) is issued only
+// when some frame of the tile is longer than 64 B (returns true).  Pieces
+// wholly past a frame get an out-of-range offset and read as zero.
+__device__ __forceinline__ bool load_window(__amdgpu_buffer_rsrc_t rs, uint32_t off, uint32_t len,
+					    uint32_t lane, u32x4 d[NPIECE], bool want_hi, uint32_t &win)
+{
+	const uint32_t q = lane & 3u, pp = lane >> 2;
+#pragma unroll
+	for (uint32_t r = 0; r < 4; ++r) {
+		const int src = (int)((16u * r + pp) << 2);
+		const uint32_t o = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)off);
+		const uint32_t L = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)len);
+		const uint32_t vo = 16u * q < L ? o + 16u * q : OOB_OFF;
+		d[r] = __builtin_amdgcn_raw_buffer_load_b128(rs, vo, 0, LOAD_AUX);
+	}
+	// phase B only when some frame is longer than 64 B and the window
+	// predictor wants bytes 64.. (want_hi); otherwise a tile with long frames
+	// stages 64 B per frame and reads the rare bytes past them from HBM
+	const bool any_long = __ballot(len > 64u) != 0ull;
+	const bool hi = any_long && want_hi;
+	win = (any_long && !hi) ? 64u : (uint32_t)WIN;
+	if (hi) {
+		const uint32_t qb = lane % NB, pb = lane / NB;
+#pragma unroll
+		for (uint32_t r = 0; r < NB; ++r) {
+			const int src = (int)(((64u / NB) * r + pb) << 2);
+			const uint32_t o = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)off);
+			const uint32_t L = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)len);
+			const uint32_t c = 16u * (4u + qb);
+			const uint32_t vo = c < L ? o + c : OOB_OFF;
+			d[4 + r] = __builtin_amdgcn_raw_buffer_load_b128(rs, vo, 0, LOAD_AUX);
+		}
+	}
+	return hi;
+}
+
+// Write a tile's loaded pieces into the transposed window: lane l holds
+// dwords 4q..4q+3 of packet p, which go to rows 4q..4q+3, column p.  With the
+// 66-dword row stride the 64 lanes of one ds_write hit distinct banks
+// (bank = 8q + 2i + p mod 32 within each 32-lane half).  Rows 16.. are
+// rewritten only when this tile has long frames, or zeroed once after a tile
+// that had them (hi_rows tracks whether they hold data).
+__device__ __forceinline__ void store_window(uint32_t *W, uint32_t lane, const u32x4 d[NPIECE],
+					     bool hi, bool &hi_rows)
+{
+	const uint32_t q = lane & 3u, pp = lane >> 2;
+#pragma unroll
+	for (uint32_t r = 0; r < 4; ++r) {
+		const uint32_t base = 4u * q * RS + 16u * r + pp;
+#pragma unroll
+		for (uint32_t i = 0; i < 4; ++i)
+			W[base + i * RS] = d[r][i];
+	}
+	if (hi) {
+		const uint32_t qb = lane % NB, pb = lane / NB;
+#pragma unroll
+		for (uint32_t r = 0; r < NB; ++r) {
+			const uint32_t base = 4u * (4u + qb) * RS + (64u / NB) * r + pb;
+#pragma unroll
+			for (uint32_t i = 0; i < 4; ++i)
+				W[base + i * RS] = d[4 + r][i];
+		}
+	} else if (hi_rows) {
+#pragma unroll
+		for (uint32_t row = 16; row < WIN / 4; ++row)
+			W[row * RS + lane] = 0u;
+	}
+	hi_rows = hi;
+}
+
+// Zero the bytes of the last loaded piece that lie past the frame
+// (frame_len .. end of its 16-B piece; loaded pieces wholly past the frame
+// read as zero already): bytes b..3 of the partial dword with one byte store
+// (b odd) and one 16-bit store (b <= 2) -- stores that are not needed go to
+// the lane's pad dword, which is zero anyway -- then the next three whole
+// dwords without a test: rows past the piece are zero (pieces past the
+// frame, or the zero rows WIN/4 .. WIN/4+2 where a frame of >= WIN bytes
+// starts).
+__device__ __forceinline__ void zero_tail(uint32_t *W, uint32_t lane, uint32_t len)
+{
+	const uint32_t pad = (WIN / 4) * RS + lane;
+	const uint32_t dw = len >> 2, b = len & 3u;
+	const bool part = b != 0u && len < WIN;
+	uint8_t *W8 = (uint8_t *)W;
+	const uint32_t pb = (dw * RS + lane) * 4u;
+	W8[(part && (b & 1u)) ? pb + b : pad * 4u + 1u] = 0;
+	*(uint16_t *)(W8 + ((part && b <= 2u) ? pb + 2u : pad * 4u + 2u)) = 0;
+	uint32_t *z = W + min((len + 3u) >> 2, (uint32_t)(WIN / 4)) * RS + lane;
+	z[0] = 0u;
+	z[RS] = 0u;
+	z[2 * RS] = 0u;
+}
+
+// Make this wave's LDS writes visible to its own later LDS reads by other
+// lanes: LDS ops of one wave complete in order, so a wave-scope fence (which
+// keeps the compiler from reordering) is all that is needed -- no block
+// barrier, waves run independently.
+__device__ __forceinline__ void wave_lds_sync()
+{
+	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+	__builtin_amdgcn_wave_barrier();
+	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// DIV = the program has rules behind rules (a CoS tree), so lanes of a wave
+// can sit on different CoS: such rounds evaluate every lane's own bit-vector
+// block at once instead of one CoS per round.
+// LT = the hot region is copied into LDS at block start (it fits the
+// budget): every per-lane table lookup is then an LDS read and the compute
+// phase issues no vector memory loads, so nothing it waits for sits behind
+// the next tile's prefetch in the (in-order) vmcnt queue.  !LT reads the hot
+// region from HBM (large rule sets).
+extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
+
+// NW = waves per block: 4 (each block copies the hot region for itself), or
+// 16 = one block per CU whose 16 waves share one LDS copy of a larger hot
+// region.  Either way 4 waves per SIMD (the VGPR budget).
+// Waves per SIMD a block shape runs at: 4-wave blocks run 4 blocks per CU,
+// the one-block-per-CU shapes NW / 4 (8 and 12 waves give each wave a
+// bigger register budget and leave LDS for a larger hot region).
+constexpr int waves_per_eu(int nw)
+{
+	return nw == 4 ? MIN_WAVES_PER_EU : nw / 4;
+}
+
+template <bool LT, bool DIV, int NW>
+__global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KArgs a)
+{
+	__shared__ uint32_t s_win[NW * RS * WROWS];
+	__shared__ uint32_t s_cnt[MAX_STATS_COS];
+	__shared__ uint32_t s_l4[256];
+
+	const uint32_t lane = threadIdx.x & (WAVE - 1);
+	const uint32_t wave = threadIdx.x >> 6;
+	uint32_t *W = s_win + wave * RS * WROWS;
+#ifdef DIAG_STAMPS
+	unsigned long long st_acc[NSTAMP] = { 0 }, st_last;
+	asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_last) :: "memory");
+#endif
+
+	const cword_t dev = (cword_t)a.dev;
+	const int32_t def_cos = (int32_t)dev[DH_DEFAULT];
+	const int32_t err_cos = (int32_t)dev[DH_ERROR];
+	const uint32_t def_valid = dev[DH_DEFAULT_VALID];
+	const uint32_t max_hops = dev[DH_MAX_HOPS];
+	const uint32_t hot_off = dev[DH_HOT_OFF];
+	const cword_t hc = dev + hot_off;                 // hot region, scalar reads
+	const cword_t prog = dev + dev[DH_PROG_OFF];
+	// the default CoS's words (the first descent round always evaluates it)
+	const cword_t dce = hc + COS_WORDS * (uint32_t)max(def_cos, 0);
+	const uint32_t d_nr = def_cos >= 0 ? dce[C_NR] : 0u;
+	const uint32_t d_bv = dce[C_BV], d_rec0 = dce[C_REC0];
+	const bool stats_on = a.stats != nullptr;
+	typedef typename std::conditional<LT, lword_t, gword_t>::type hot_t;
+	hot_t H;
+	// first descriptors before the hot-region copy: their latency overlaps it
+	const uint32_t nt = (a.n + WAVE - 1) / WAVE;
+	const uint32_t tstride = gridDim.x * NW;
+	uint32_t tile = blockIdx.x * NW + wave;
+	uint32_t d_off = 0, d_len = 0, n_off = 0, n_len = 0;
+	{
+		const uint32_t p0 = tile * WAVE + lane, p1 = (tile + tstride) * WAVE + lane;
+		if (tile < nt && p0 < a.n) {
+			d_off = a.off[p0];
+			d_len = a.len[p0];
+		}
+		if (tile + tstride < nt && p1 < a.n) {
+			n_off = a.off[p1];
+			n_len = a.len[p1];
+		}
+	}
+	// Software pipeline over this wave's tiles (64 packets each): while tile
+	// t is parsed and classified, tile t+1's header windows are in flight
+	// into registers (load_window) and tile t+2's descriptors are being
+	// fetched.  Tile t's result records are stored at the top of iteration
+	// t+1, before tile t+2's loads are issued, so waiting for window data
+	// never waits behind a younger store (vmcnt retires in order), and the
+	// records are not held in registers through parse and classify.
+	const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+		(void *)a.pkts, (short)0, (int)OOB_OFF, 0x00020000);
+	u32x4 d[NPIECE];
+	bool d_hi, hi_rows = true;
+	// window predictor: stage bytes 64..WIN-1 of long frames only while the
+	// frames of the last parsed tile needed them (the fields of its rule
+	// program and its parse reach past byte 64); the first tiles stage them
+#if defined(DIAG_FORCE_LO)
+	bool want_hi = false;     // diagnostic: 64-B windows from the first tile
+#elif defined(DIAG_FORCE_HI)
+	bool want_hi = true;
+#else
+	bool want_hi = a.hint == nullptr || *(const uint32_t *)a.hint + 1u == a.seq;
+#endif
+	bool saw_hi = false;
+	uint32_t d_win = WIN, my_win = WIN;
+	const uint32_t p_l3end = dev[DH_L3END], p_l4end = dev[DH_L4END], p_frend = dev[DH_FREND];
+	// the first tile's windows are in flight during the block setup below
+	if (tile < nt)
+		d_hi = load_window(rs, d_off, d_len, lane, d, want_hi, d_win);
+	if constexpr (LT) {
+		// hot region -> LDS in 16-B pieces (the device program and the
+		// dynamic LDS size are padded to 16 B)
+		const uint32_t hq = (dev[DH_HOT_WORDS] + 3u) >> 2;
+		typedef const __attribute__((address_space(1))) u32x4 *gvec_t;
+		const gvec_t src = (gvec_t)(a.dev + hot_off);
+		u32x4 *dst = (u32x4 *)s_dyn;
+		for (uint32_t i = threadIdx.x; i < hq; i += NW * WAVE)
+			dst[i] = src[i];
+		H = (lword_t)s_dyn;
+	} else {
+		H = (gword_t)(a.dev + hot_off);
+	}
+
+	if (stats_on) {
+		for (uint32_t i = threadIdx.x; i < MAX_STATS_COS; i += NW * WAVE)
+			s_cnt[i] = 0;
+	}
+	for (uint32_t i = threadIdx.x; i < 256u; i += NW * WAVE)
+		s_l4[i] = c_l4tab.v[i];
+	for (uint32_t r = WIN / 4; r < WROWS; ++r)
+		W[r * RS + lane] = 0u;   // pad / zero rows: always zero
+	__syncthreads();
+	STAMP(5);   // block setup (hot-region copy) done
+
+	uint4 prev_rec = make_uint4(0, 0, 0, 0);
+	uint32_t prev_pi = 0;
+	bool prev_valid = false;
+	for (; tile < nt; tile += tstride) {
+		const uint32_t pi = tile * WAVE + lane;
+		const bool valid = pi < a.n;
+		if (!PREFETCH && tile != blockIdx.x * NW + wave) {
+			d_off = valid ? a.off[pi] : 0u;
+			d_len = valid ? (uint32_t)a.len[pi] : 0u;
+			d_hi = load_window(rs, d_off, d_len, lane, d, want_hi, d_win);
+		}
+		const uint32_t my_off = d_off, my_len = d_len;
+		my_win = d_win;
+
+		wave_lds_sync();   // previous tile's window reads are done
+		store_window(W, lane, d, d_hi, hi_rows);
+		zero_tail(W, lane, my_len);   // same wave: LDS stores stay in order
+		// previous tile's records: issued before this tile's prefetch, so the
+		// next wait for window data never waits behind a younger store
+		if (prev_valid)
+			*(uint4 *)(a.out + prev_pi) = prev_rec;
+		prev_valid = false;
+
+		STAMP(0);   // data of this tile landed in LDS
+		// advance the pipeline: data of tile+stride, descriptors of tile+2*stride
+		if (PREFETCH) {
+			d_off = n_off;
+			d_len = n_len;
+			const uint32_t t2 = tile + 2u * tstride, p2 = t2 * WAVE + lane;
+			n_off = 0;
+			n_len = 0;
+			if (t2 < nt && p2 < a.n) {
+				n_off = a.off[p2];
+				n_len = a.len[p2];
+			}
+			// no loads for a tile past the end (its registers would be
+			// waited for before reuse after the loop)
+			if (tile + tstride < nt)
+				d_hi = load_window(rs, d_off, d_len, lane, d, want_hi, d_win);
+		}
+		wave_lds_sync();
+#ifdef DIAG_STAGEONLY
+		if (valid) {
+			uint4 rec;
+			rec.x = W[3 * RS + lane] ^ W[8 * RS + lane];
+			rec.y = my_len;
+			rec.z = 0;
+			rec.w = 0;
+			*(uint4 *)(a.out + pi) = rec;
+		}
+		continue;
+#endif
+
+		Pkt k;
+		k.w = W + lane;
+		k.g = a.pkts + my_off;
+		k.len = my_len;
+		k.win = my_win;
+
+		STAMP(1);   // next tile's loads issued
+		Parsed p;
+		if (a.opt == 0u) {
+			bool slow;
+			p = parse_fast(k, s_l4, slow);
+			if (__ballot(slow) != 0ull) {
+				if (slow)
+					p = parse_packet(k, 0u);
+			}
+		} else {
+			// pktin checksum / drop options: the general parser for every
+			// lane, then the L4 checksums (whole frames from HBM)
+			p = parse_packet(k, a.opt);
+			if (a.opt & OPT_L4_CK)
+				l4_chksum(k, p, a.opt, rs, my_off);
+		}
+		const Fields x = fields_of(k, p);
+		{
+			// bytes this tile's lanes use: the parse's L3 / L4 headers and the
+			// program's fields (conservative: gates ignored)
+			const uint32_t l4h = (p.flags & F_TCP) ? 13u : ((p.flags & F_UDP) ? 6u : 0u);
+			uint32_t need = p_frend;
+			need = max(need, p.l3 != 0xFFFFu ? p.l3 + max(p_l3end, (p.flags & F_IPV6) ? 40u : 20u) : 0u);
+			need = max(need, p.l4 != 0xFFFFu ? p.l4 + max(p_l4end, l4h) : 0u);
+#ifdef DIAG_FORCE_HI
+			want_hi = true;
+#else
+			want_hi = a.opt != 0u || __ballot(valid && my_len > 64u && need > 64u) != 0ull;
+#endif
+			saw_hi = saw_hi || want_hi;
+		}
+#ifdef DIAG_PARSEONLY
+		if (valid) {
+			uint4 rec;
+			rec.x = p.flags;
+			rec.y = p.err;
+			rec.z = x.f ^ x.l4;
+			rec.w = (p.l3 & 0xffffu) | ((p.l4 & 0xffffu) << 16);
+			*(uint4 *)(a.out + pi) = rec;
+		}
+		continue;
+#endif
+
+		// ---- select the starting CoS (cls_select_cos, odp_classification.c:1694-1726)
+		// Per-lane state is kept in integers updated by selects: bools live
+		// across the descent loop would become lane masks merged at every
+		// join (and spill SGPRs).
+		const bool ok_parse = valid && p.ret >= 0;
+		const bool perr = p.err != 0u;
+		int32_t cur = perr ? err_cos : def_cos;
+		uint32_t pend = (ok_parse && !perr && def_cos >= 0 && def_valid) ? 1u : 0u;
+
+		STAMP(2);   // parsed, start CoS selected
+		// ---- CoS descent (match_pmr_cos, :1624-1667).  Each round moves
+		// pending lanes one hop: the CoS of the first pending lane is
+		// evaluated by every lane sitting on it (bit-vector or linear engine,
+		// the CoS's words in SGPRs); in tree programs (DIV) lanes on other
+		// bit-vector CoS evaluate their own blocks in the same round.
+		uint32_t hops = 0, mark = 0, matched = 0, loop = 0;
+		// one hop of the lanes in `proc` whose evaluation gave hit / nxt / ..
+		auto advance = [&](uint32_t proc, uint32_t hit, uint32_t nxt, uint32_t nmark,
+				   uint32_t nleaf) {
+			const uint32_t take = proc & hit;
+			cur = take ? (int32_t)nxt : cur;
+			mark = take ? nmark : mark;
+			matched |= take;
+			hops += take;
+			const uint32_t lp = (take != 0u && hops > max_hops) ? 1u : 0u;
+			loop |= lp;
+			// still pending: a rule matched, under the hop limit, and the
+			// destination CoS has rules
+			pend = proc ? ((take != 0u && lp == 0u && nleaf == 0u) ? 1u : 0u) : pend;
+			if (stats_on) {
+				if (take != 0u && stats_bit(a, nxt))
+					atomicAdd(&s_cnt[nxt], 1u);
+			}
+		};
+		// round 1: every pending lane sits on the default CoS, whose words
+		// are loop-invariant (d_nr / d_bv / d_rec0, loaded once per wave)
+		if (__ballot(pend != 0u) != 0ull) {
+			uint32_t hit = 0, nleaf = 0, nxt = 0, nmark = 0;
+			const bool g = pend != 0u;
+			if (d_bv != 0u && d_nr != 0u)
+				bv_eval(DescU{ hc + d_bv }, H, g, k, p, x, hit, nxt, nmark, nleaf);
+			else
+				linear_scan(prog, d_rec0, d_nr, g, k, p, x, hit, nxt, nmark);
+			advance(g ? 1u : 0u, hit, nxt, nmark, nleaf);
+		}
+		for (;;) {
+			const unsigned long long pm = __ballot(pend != 0u);
+			if (pm == 0ull)
+				break;
+			uint32_t hit = 0, nleaf = 0, nxt = 0, nmark = 0, handled = 0;
+			bool act = pend != 0u;
+			if constexpr (DIV) {
+				const int32_t c0 = __builtin_amdgcn_readlane(cur, (int)__builtin_ctzll(pm));
+				if (__ballot(pend != 0u && cur != c0) != 0ull) {
+					const uint32_t ci = COS_WORDS * (uint32_t)(pend != 0u ? cur : c0);
+					const uint32_t my_nr = H[ci + C_NR];
+					const uint32_t my_bv = H[ci + C_BV];
+					const bool empty = pend != 0u && my_nr == 0u;
+					const bool bvl = pend != 0u && my_nr != 0u && my_bv != 0u;
+					if (__ballot(bvl))
+						bv_eval(DescL<hot_t>{ H, my_bv }, H, bvl, k, p, x, hit, nxt, nmark,
+							nleaf);
+					handled = (bvl || empty) ? 1u : 0u;
+					act = pend != 0u && handled == 0u;
+				}
+			}
+			uint32_t grp = 0;
+			const unsigned long long am = __ballot(act);
+			if (am) {
+				const int32_t c1 = __builtin_amdgcn_readlane(cur, (int)__builtin_ctzll(am));
+				const bool g = act && cur == c1;
+				grp = g ? 1u : 0u;
+				const cword_t ce = hc + COS_WORDS * (uint32_t)c1;
+				const uint32_t nr = ce[C_NR], bv = ce[C_BV];
+				if (bv != 0u && nr != 0u)
+					bv_eval(DescU{ hc + bv }, H, g, k, p, x, hit, nxt, nmark, nleaf);
+				else
+					linear_scan(prog, ce[C_REC0], nr, g, k, p, x, hit, nxt, nmark);
+			}
+			advance(handled | grp, hit, nxt, nmark, nleaf);
+		}
+
+		STAMP(3);   // descent done
+#ifdef DIAG_DESCENTONLY
+		if (valid) {
+			uint4 rec;
+			rec.x = (uint32_t)cur;
+			rec.y = mark;
+			rec.z = hops | (matched << 8) | (loop << 9);
+			rec.w = p.flags;
+			*(uint4 *)(a.out + pi) = rec;
+		}
+		continue;
+#endif
+		// ---- final CoS -> outcome / queue (_odp_cls_classify_packet, :1742-1771)
+		const bool mk = matched != 0u && loop == 0u;
+		const uint32_t flags = mk ? ((p.flags & ~F_CLS_MARK) | (mark ? F_CLS_MARK : 0u)) : p.flags;
+		const uint32_t out_mark = (mk && mark) ? mark : 0u;
+		const bool live = ok_parse && loop == 0u;
+		// error CoS, the CoS the descent ended on, or the default CoS
+		const bool to_cur = !perr && matched != 0u && cur != def_cos;
+		const int32_t fc = perr ? err_cos : (to_cur ? cur : def_cos);
+		if (stats_on) {
+			if (live && !to_cur && fc >= 0 && stats_bit(a, (uint32_t)fc))
+				atomicAdd(&s_cnt[fc], 1u);
+		}
+		const uint32_t meta = H[COS_WORDS * (uint32_t)max(fc, 0) + C_META];
+		const bool have = live && fc >= 0;
+		const bool drop = (meta & 0xffu) != 0u;
+		const uint32_t outcome = !valid ? MI_CLS_OUT_DISCARD
+			: (p.ret < 0 ? MI_CLS_OUT_PARSE_DROP
+			: (loop ? MI_CLS_OUT_LOOP
+			: (fc < 0 ? MI_CLS_OUT_DISCARD
+			: (drop ? MI_CLS_OUT_COS_DROP : MI_CLS_OUT_ENQ))));
+		const uint32_t cos_idx = have ? (meta >> 24) : 0xFFu;
+		const uint32_t nq = (meta >> 8) & 0xffu;
+		const bool hq = have && !drop && nq > 1u;
+		uint32_t queue = 0;
+		if (__ballot(hq) != 0ull) {
+			if (hq)
+				queue = (rss_hash(k, p, (meta >> 16) & 0xffu) & 31u) % nq;
+		}
+		hops = loop ? 0xFFu : hops;
+
+		prev_rec.x = flags;
+		prev_rec.y = (p.err & 0xffu) | ((outcome & 0xffu) << 8) | ((cos_idx & 0xffu) << 16) |
+			     ((hops & 0xffu) << 24);
+		prev_rec.z = (queue & 0xffffu) | ((out_mark & 0xffffu) << 16);
+		prev_rec.w = (p.l3 & 0xffffu) | ((p.l4 & 0xffffu) << 16);
+		prev_pi = pi;
+		prev_valid = valid;
+		STAMP(4);   // outcome computed, record stored
+	}
+	STAMP(7);   // loop left
+	if (prev_valid)
+		*(uint4 *)(a.out + prev_pi) = prev_rec;
+	// the waves of block 0 are the sample that sets the hint: stores to one
+	// address serialise, so never one per wave
+	if (saw_hi && a.hint && lane == 0 && blockIdx.x == 0)
+		*a.hint = a.seq;
+	STAMP(6);   // last record issued
+#ifdef DIAG_STAMPS
+	if (lane == 0 && a.diag) {
+		for (int i = 0; i < NSTAMP; ++i)
+			atomicAdd(a.diag + i, st_acc[i]);
+		atomicAdd(a.diag + NSTAMP, 1ull);
+	}
+#endif
+
+	if (stats_on) {
+		__syncthreads();
+		for (uint32_t i = threadIdx.x; i < MAX_STATS_COS; i += NW * WAVE)
+			if (s_cnt[i])
+				atomicAdd(a.stats + i, (unsigned long long)s_cnt[i]);
+	}
+}
+
+
+// Launch one instantiation of the kernel for block shape NW (defined in
+// mi_cls_k<NW>.hip).
+int mi_cls_launch_k4(bool lt, bool div, unsigned grid, size_t dyn, hipStream_t st, const KArgs &a);
+int mi_cls_launch_k8(bool lt, bool div, unsigned grid, size_t dyn, hipStream_t st, const KArgs &a);
+int mi_cls_launch_k12(bool lt, bool div, unsigned grid, size_t dyn, hipStream_t st, const KArgs &a);
+int mi_cls_launch_k16(bool lt, bool div, unsigned grid, size_t dyn, hipStream_t st, const KArgs &a);

@@ -1,0 +1,13 @@
+// mi_cls_k12.hip -- the 12-wave block shape of mi_cls_kernel (one
+// translation unit per shape so the shapes compile in parallel).
+#include "mi_cls_dev.h"
+
+int mi_cls_launch_k12(bool lt, bool div, unsigned grid, size_t dyn, hipStream_t st, const KArgs &a)
+{
+	(void)lt;   // 12-wave blocks exist for LDS-resident hot regions only
+	if (div)
+		hipLaunchKernelGGL((mi_cls_kernel<true, true, 12>), dim3(grid), dim3(12 * WAVE), dyn, st, a);
+	else
+		hipLaunchKernelGGL((mi_cls_kernel<true, false, 12>), dim3(grid), dim3(12 * WAVE), dyn, st, a);
+	return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
