@@ -223,8 +223,9 @@ int mi_cls_stats_reset(mi_cls_ctx_t *ctx);
  * device encoding and describe it.  info[0] total 32-bit words, [1] words of
  * the per-lane "hot" region (copied to LDS when it fits), [2] CoS with a
  * classification block, [3..6] blocks per engine (direct, candidate,
- * bitmap, wide bitmap), [7] 1 if some rule leads to a CoS with rules.
- * n >= 8.  Used by tests and tools to check engine selection on the CPU. */
+ * bitmap, wide bitmap), [7] 1 if some rule leads to a CoS with rules,
+ * [8] single-candidate blocks.  n >= 9.  Used by tests and tools to check
+ * engine selection on the CPU. */
 int mi_cls_program_info(const void *tbl, size_t bytes, uint32_t *info, uint32_t n);
 
 /* Last error string for the context (static storage, never NULL). */

@@ -267,13 +267,13 @@ class Classifier:
     def program_info(self) -> dict:
         """Device encoding of the current rule snapshot (host only)."""
         blob = self.compile()
-        info = (C.c_uint32 * 8)()
-        rc = self.L.mi_cls_program_info(blob, len(blob), info, 8)
+        info = (C.c_uint32 * 9)()
+        rc = self.L.mi_cls_program_info(blob, len(blob), info, 9)
         if rc:
             raise RuntimeError(f"mi_cls_program_info: {rc}")
         return {"words": info[0], "hot_words": info[1], "blocks": info[2],
                 "direct": info[3], "candidate": info[4], "bitmap": info[5], "wide": info[6],
-                "tree": bool(info[7])}
+                "tree": bool(info[7]), "cand1": info[8]}
 
     # -- data path -------------------------------------------------------
     def classify_device(self, d_buf, d_off, d_len, n, d_out, stream=0):

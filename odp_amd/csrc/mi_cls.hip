@@ -13,6 +13,8 @@ struct mi_cls_ctx {
 	int loaded;
 	uint32_t hot_words;      // size of the program's hot region
 	int tree;                // some rule leads to a CoS with rules (DIV kernel)
+	int flat_mode;           // engine of the default CoS block when every packet is
+	                         // decided there in one round (flat kernels), else -1
 	int wpb;                 // forced waves per block (MI_CLS_WPB at load), 0 = auto
 	uint32_t opt;            // pktin options (mi_cls_pktin_opt_set)
 	unsigned long long *d_stats;
@@ -421,10 +423,32 @@ static bool build_bv(const mi_cos_t *cs, const mi_rule_t *rs, const mi_term_t *t
 			if ((tmask[r] >> c) & 1u)
 				freq[c][want[r][c]]++;
 	}
-	// MI_CLS_NO_WIDE: candidate lists instead of wide rows (A/B, tests)
+	// primary class of every alive constrained rule: the class whose value
+	// the fewest alive rules share (candidate engines file the rule under it)
+	std::vector<uint32_t> prim_of(nrules, BV_NONE);
+	std::vector<std::map<Key4, uint32_t>> filed(ncls);   // value -> #rules filed
+	uint32_t max_list = 0, prim_mask = 0;
+	for (uint32_t r = 0; r < nrules; ++r) {
+		if (!alive[r] || tmask[r] == 0u)
+			continue;
+		uint32_t best = 0xFFFFFFFFu;
+		for (uint32_t c = 0; c < ncls; ++c)
+			if (((tmask[r] >> c) & 1u) && freq[c][want[r][c]] < best) {
+				best = freq[c][want[r][c]];
+				prim_of[r] = c;
+			}
+		const uint32_t c = prim_of[r];
+		max_list = std::max(max_list, ++filed[c][want[r][c]]);
+		prim_mask |= 1u << c;
+	}
+	// MI_CLS_NO_WIDE: candidate lists instead of wide rows; MI_CLS_NO_CAND1:
+	// no single-candidate engine (A/B, tests)
 	const bool wide_ok = getenv("MI_CLS_NO_WIDE") == nullptr;
+	const bool cand1_ok = getenv("MI_CLS_NO_CAND1") == nullptr;
 	const uint32_t mode = ncls == 1 ? 0u
-		: (nrules <= 32 ? 2u : ((wide_ok && nrules <= 32 * BV_WIDE_WORDS) ? 3u : 1u));
+		: (nrules <= 32 ? 2u
+		: ((cand1_ok && max_list <= 1u && nrules < 0xFFFFu) ? 4u
+		: ((wide_ok && nrules <= 32 * BV_WIDE_WORDS) ? 3u : 1u)));
 	std::vector<std::map<Key4, uint32_t>> kid(ncls);   // value -> key id (1..)
 	for (uint32_t c = 0; c < ncls; ++c) {
 		uint32_t id = 1;
@@ -504,6 +528,34 @@ static bool build_bv(const mi_cos_t *cs, const mi_rule_t *rs, const mi_term_t *t
 		for (uint32_t h = 0; h < 2; ++h)
 			for (uint32_t j = 0; j < R; ++j)
 				blk.insert(blk.end(), rows[j]->begin() + 4 * h, rows[j]->begin() + 4 * h + 4);
+	} else if (mode == 4u) {
+		// single-candidate records, 16-B aligned, RW = 1 + ncls rounded up
+		// to 4 words: w0 = constrained-class mask (bit 31: never holds),
+		// w[1 + c] = what class c must be: the masked value (one-word
+		// classes) or the key id (longer keys)
+		const uint32_t RW = (1u + ncls + 3u) & ~3u;
+		align4();
+		blk[4] = base + (uint32_t)blk.size();
+		blk[5] = RW;
+		uint32_t lk = prim_mask;
+		for (uint32_t c = 0; c < ncls; ++c)
+			if (cls_list[c].nkey > 1u)
+				lk |= 1u << c;   // key ids for the record compare
+		blk[6] = lk;
+		blk[7] = prim_mask;
+		for (uint32_t r = 0; r < nrules; ++r) {
+			std::vector<uint32_t> rec(RW, 0);
+			if (alive[r]) {
+				rec[0] = tmask[r];
+				for (uint32_t c = 0; c < ncls; ++c)
+					if ((tmask[r] >> c) & 1u)
+						rec[1 + c] = cls_list[c].nkey == 1u ? want[r][c][0]
+										 : kid[c][want[r][c]];
+			} else {
+				rec[0] = 0x80000000u;
+			}
+			blk.insert(blk.end(), rec.begin(), rec.end());
+		}
 	} else if (mode == 1u) {
 		const uint32_t RW = 1u + (ncls + 1u) / 2u;
 		blk[4] = base + (uint32_t)blk.size();
@@ -618,6 +670,13 @@ static bool build_bv(const mi_cos_t *cs, const mi_rule_t *rs, const mi_term_t *t
 				val = row_of(c, &keys[i]);   // non-zero: the key's own rules
 			} else if (mode == 3u) {
 				val = base + rows_at + 4u * key_row[c][i];   // word index, non-zero
+			} else if (mode == 4u) {
+				// key id << 16 | 1 + the rule filed under this key (0: none)
+				uint32_t cand = 0;
+				for (uint32_t r = 0; r < nrules && !cand; ++r)
+					if (prim_of[r] == c && want[r][c] == keys[i])
+						cand = r + 1u;
+				val = (kid[c][keys[i]] << 16) | cand;
 			} else {
 				const uint32_t id = kid[c][keys[i]];
 				uint32_t off = 0;
@@ -749,11 +808,12 @@ static int assemble(const void *tbl, uint32_t **out, size_t *out_words)
 // Host-only introspection of the device encoding a table assembles into (no
 // device needed): info[0] total words, [1] hot-region words, [2] CoS with a
 // classification block, [3..6] blocks per mode (direct, candidate, bitmap,
-// wide), [7] 1 if the program is a tree (DIV kernel).  Tests and tools use it
+// wide), [7] 1 if the program is a tree (DIV kernel), [8] single-candidate
+// blocks.  Tests and tools use it
 // to check the engine choice on the CPU.
 extern "C" int mi_cls_program_info(const void *tbl, size_t bytes, uint32_t *info, uint32_t n)
 {
-	if (!info || n < 8)
+	if (!info || n < 9)
 		return -EINVAL;
 	int rc = validate_tbl(tbl, bytes);
 	if (rc)
@@ -772,7 +832,8 @@ extern "C" int mi_cls_program_info(const void *tbl, size_t bytes, uint32_t *info
 		const uint32_t bv = hot[COS_WORDS * s + C_BV];
 		if (bv) {
 			info[2]++;
-			info[3 + (hot[bv] & 3u)]++;
+			const uint32_t md = hot[bv];
+			info[md == 4u ? 8u : 3u + (md & 3u)]++;
 		}
 	}
 	const mi_cos_t *tc = (const mi_cos_t *)((const uint8_t *)tbl + th->cos_off);
@@ -815,6 +876,25 @@ extern "C" int mi_cls_rules_load(mi_cls_ctx_t *c, const void *tbl, size_t bytes,
 		e = getenv("MI_CLS_WPB");
 		c->wpb = e ? atoi(e) : 0;
 	}
+	int flat_mode = -1;
+	{
+		// flat program: the default CoS has a classification block and all
+		// its rules lead to CoS without rules (one round decides every
+		// packet); MI_CLS_NO_FLAT disables the flat kernels (A/B, tests)
+		const mi_tbl_hdr_t *th = (const mi_tbl_hdr_t *)tbl;
+		const mi_cos_t *tc = (const mi_cos_t *)((const uint8_t *)tbl + th->cos_off);
+		const mi_rule_t *tr = (const mi_rule_t *)((const uint8_t *)tbl + th->rule_off);
+		const int32_t d = th->default_cos;
+		if (d >= 0 && th->default_valid && tc[d].num_rules && !getenv("MI_CLS_NO_FLAT")) {
+			const uint32_t *hot = w + w[DH_HOT_OFF];
+			const uint32_t bv = hot[COS_WORDS * (uint32_t)d + C_BV];
+			bool leaves = true;
+			for (uint32_t r = 0; r < tc[d].num_rules && leaves; ++r)
+				leaves = tc[tr[tc[d].rule_begin + r].dst_cos].num_rules == 0;
+			if (bv && leaves && hot[bv] != 1u)
+				flat_mode = (int)hot[bv];
+		}
+	}
 	if (getenv("MI_CLS_VERBOSE"))
 		fprintf(stderr, "mi_cls: program %zu words, hot region %u words\n", words, hot_words);
 	size_t nbytes = words * sizeof(uint32_t);
@@ -843,6 +923,7 @@ extern "C" int mi_cls_rules_load(mi_cls_ctx_t *c, const void *tbl, size_t bytes,
 		return -EIO;
 	c->hot_words = hot_words;
 	c->tree = tree;
+	c->flat_mode = flat_mode;
 	c->loaded = 1;
 	return 0;
 }
@@ -939,8 +1020,10 @@ extern "C" int mi_cls_classify(mi_cls_ctx_t *c, const uint8_t *pkts, const uint3
 	uint32_t grid = tiles < max_grid ? tiles : max_grid;
 	const size_t dyn = lt ? hot_bytes : 0;
 	hipStream_t st = (hipStream_t)stream;
-int lrc;
-	if (nw == 16)
+	int lrc;
+	if (c->flat_mode >= 0 && c->opt == 0 && lt && (nw == 4 || nw == 12 || nw == 16))
+		lrc = mi_cls_launch_flat(nw, c->flat_mode, grid, dyn, st, a);
+	else if (nw == 16)
 		lrc = mi_cls_launch_k16(lt, div, grid, dyn, st, a);
 	else if (nw == 12)
 		lrc = mi_cls_launch_k12(lt, div, grid, dyn, st, a);

@@ -1091,12 +1091,14 @@ __device__ __forceinline__ uint32_t bv_lookup(const D &cr, T H, const uint32_t k
 // uniform or per lane); H is the hot region the block's offsets index.  On
 // return, lanes of `act` with a matching rule have hit = 1 and the rule's
 // destination CoS / mark / leaf bit in nxt / nmark / nleaf.
-template <typename D, typename T>
+// FM >= 0: the block's engine is known at compile time (the flat-program
+// kernels); -1: read from the block.
+template <int FM = -1, typename D, typename T>
 __device__ __forceinline__ void bv_eval(const D &blk, T H, bool act, const Pkt &k, const Parsed &p,
 					const Fields &x, uint32_t &hit, uint32_t &nxt, uint32_t &nmark,
 					uint32_t &nleaf)
 {
-	const uint32_t mode = blk(0), ncls = blk(1), res = blk(2);
+	const uint32_t mode = FM >= 0 ? (uint32_t)FM : blk(0), ncls = blk(1), res = blk(2);
 	uint32_t first = BV_NONE;
 	if (mode == 0u) {
 		// direct: one class, the slot holds 1 + the first live rule of its
@@ -1152,6 +1154,59 @@ __device__ __forceinline__ void bv_eval(const D &blk, T H, bool act, const Pkt &
 #pragma unroll
 		for (int i = (int)BV_WIDE_WORDS - 1; i >= 0; --i)
 			first = acc[i] != 0u ? 32u * (uint32_t)i + (uint32_t)__builtin_ctz(acc[i]) : first;
+	} else if (mode == 4u) {
+		// single candidate per primary key: lookups only for the classes
+		// rules are filed under (and longer-key classes, for their key
+		// ids); each hit names the one rule filed under the packet's key,
+		// whose record is checked against the packet's keys of every class
+		// it constrains; the smallest holding candidate wins
+		const uint32_t rec0 = blk(4), rw = blk(5), lk = blk(6), pm = blk(7);
+		uint32_t cmpv[BV_MAX_CLS], cand[BV_MAX_CLS], prm = 0;
+		first = blk(3);   // the first rule without a classified term
+#pragma unroll
+		for (uint32_t kc = 0; kc < BV_MAX_CLS; ++kc) {
+			cmpv[kc] = 0u;
+			cand[kc] = 0u;
+			if (kc < ncls) {
+				const D cr = blk.at(8u + BV_CLS_WORDS * kc);
+				uint32_t key[4];
+				const bool present = bv_key(cr, k, p, x, key);
+				prm |= present ? 1u << kc : 0u;
+				cmpv[kc] = key[0];
+				if ((lk >> kc) & 1u) {
+					const uint32_t v = bv_lookup(cr, H, key, act && present);
+					cand[kc] = ((pm >> kc) & 1u) ? (v & 0xffffu) : 0u;
+					cmpv[kc] = cr(1) == 1u ? key[0] : (v >> 16);
+				}
+			}
+		}
+#pragma unroll
+		for (uint32_t kc = 0; kc < BV_MAX_CLS; ++kc) {
+			if (kc < ncls && ((pm >> kc) & 1u)) {
+				const uint32_t c1 = cand[kc];
+				const bool tr = act && c1 != 0u && c1 - 1u < first;
+				if (__ballot(tr) != 0ull) {
+					const uint32_t ra = rec0 + (tr ? c1 - 1u : 0u) * rw;
+					const u32x4 q0 = ld4(H, ra);
+					u32x4 q1 = { 0u, 0u, 0u, 0u }, q2 = { 0u, 0u, 0u, 0u };
+					if (rw > 4u)
+						q1 = ld4(H, ra + 4u);
+					if (rw > 8u)
+						q2 = ld4(H, ra + 8u);
+					const uint32_t tm = q0[0];
+					bool ok = (tm >> 31) == 0u;
+#pragma unroll
+					for (uint32_t c2 = 0; c2 < BV_MAX_CLS; ++c2) {
+						if (c2 < ncls) {
+							const uint32_t w = c2 < 3u ? q0[1 + c2] : (c2 < 7u ? q1[c2 - 3u] : q2[0]);
+							const bool need = (tm >> c2) & 1u;
+							ok = ok && (!need || (((prm >> c2) & 1u) && cmpv[c2] == w));
+						}
+					}
+					first = (tr && ok) ? c1 - 1u : first;
+				}
+			}
+		}
 	} else {
 		// candidate: key id per class, then the candidates' records
 		const uint32_t rec0 = blk(4), rw = blk(5);
@@ -1429,7 +1484,12 @@ constexpr int waves_per_eu(int nw)
 	return nw == 4 ? MIN_WAVES_PER_EU : nw / 4;
 }
 
-template <bool LT, bool DIV, int NW>
+// FM >= 0: flat-program kernel -- every pending lane is decided in round 1
+// on the default CoS, whose block uses engine FM (all its rules lead to CoS
+// without rules), and no pktin option is set: no descent loop, no linear
+// scan, no checksum path in the code (fewer registers, straight-line
+// engine).  The host picks it only for such programs (mi_cls_classify).
+template <bool LT, bool DIV, int NW, int FM = -1>
 __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KArgs a)
 {
 	__shared__ uint32_t s_win[NW * RS * WROWS];
@@ -1588,14 +1648,14 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 
 		STAMP(1);   // next tile's loads issued
 		Parsed p;
-		if (a.opt == 0u) {
+		if (FM >= 0 || a.opt == 0u) {
 			bool slow;
 			p = parse_fast(k, s_l4, slow);
 			if (__ballot(slow) != 0ull) {
 				if (slow)
 					p = parse_packet(k, 0u);
 			}
-		} else {
+		} else if constexpr (FM < 0) {
 			// pktin checksum / drop options: the general parser for every
 			// lane, then the L4 checksums (whole frames from HBM)
 			p = parse_packet(k, a.opt);
@@ -1668,13 +1728,17 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 		if (__ballot(pend != 0u) != 0ull) {
 			uint32_t hit = 0, nleaf = 0, nxt = 0, nmark = 0;
 			const bool g = pend != 0u;
-			if (d_bv != 0u && d_nr != 0u)
-				bv_eval(DescU{ hc + d_bv }, H, g, k, p, x, hit, nxt, nmark, nleaf);
-			else
-				linear_scan(prog, d_rec0, d_nr, g, k, p, x, hit, nxt, nmark);
+			if constexpr (FM >= 0) {
+				bv_eval<FM>(DescU{ hc + d_bv }, H, g, k, p, x, hit, nxt, nmark, nleaf);
+			} else {
+				if (d_bv != 0u && d_nr != 0u)
+					bv_eval(DescU{ hc + d_bv }, H, g, k, p, x, hit, nxt, nmark, nleaf);
+				else
+					linear_scan(prog, d_rec0, d_nr, g, k, p, x, hit, nxt, nmark);
+			}
 			advance(g ? 1u : 0u, hit, nxt, nmark, nleaf);
 		}
-		for (;;) {
+		for (; FM < 0;) {
 			const unsigned long long pm = __ballot(pend != 0u);
 			if (pm == 0ull)
 				break;
@@ -1793,3 +1857,6 @@ int mi_cls_launch_k4(bool lt, bool div, unsigned grid, size_t dyn, hipStream_t s
 int mi_cls_launch_k8(bool lt, bool div, unsigned grid, size_t dyn, hipStream_t st, const KArgs &a);
 int mi_cls_launch_k12(bool lt, bool div, unsigned grid, size_t dyn, hipStream_t st, const KArgs &a);
 int mi_cls_launch_k16(bool lt, bool div, unsigned grid, size_t dyn, hipStream_t st, const KArgs &a);
+// flat-program kernels (FM = engine of the default CoS block; NW 4, 12, 16;
+// hot region in LDS): mi_cls_kf.hip
+int mi_cls_launch_flat(int nw, int fm, unsigned grid, size_t dyn, hipStream_t st, const KArgs &a);

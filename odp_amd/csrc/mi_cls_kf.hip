@@ -1,0 +1,38 @@
+// mi_cls_kf.hip -- flat-program instantiations of mi_cls_kernel: the default
+// CoS decides every packet in one round with a compile-time engine (direct,
+// bitmap, wide bitmap, single candidate), hot region in LDS, no pktin
+// options.  One translation unit so they compile beside the general shapes.
+#include "mi_cls_dev.h"
+
+template <int NW>
+static int launch_fm(int fm, unsigned grid, size_t dyn, hipStream_t st, const KArgs &a)
+{
+	switch (fm) {
+	case 0:
+		hipLaunchKernelGGL((mi_cls_kernel<true, false, NW, 0>), dim3(grid), dim3(NW * WAVE), dyn, st, a);
+		break;
+	case 2:
+		hipLaunchKernelGGL((mi_cls_kernel<true, false, NW, 2>), dim3(grid), dim3(NW * WAVE), dyn, st, a);
+		break;
+	case 3:
+		hipLaunchKernelGGL((mi_cls_kernel<true, false, NW, 3>), dim3(grid), dim3(NW * WAVE), dyn, st, a);
+		break;
+	case 4:
+		hipLaunchKernelGGL((mi_cls_kernel<true, false, NW, 4>), dim3(grid), dim3(NW * WAVE), dyn, st, a);
+		break;
+	default:
+		return -EINVAL;
+	}
+	return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+int mi_cls_launch_flat(int nw, int fm, unsigned grid, size_t dyn, hipStream_t st, const KArgs &a)
+{
+	if (nw == 16)
+		return launch_fm<16>(fm, grid, dyn, st, a);
+	if (nw == 12)
+		return launch_fm<12>(fm, grid, dyn, st, a);
+	if (nw == 4)
+		return launch_fm<4>(fm, grid, dyn, st, a);
+	return -EINVAL;
+}

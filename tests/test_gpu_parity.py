@@ -24,6 +24,9 @@ ENGINE_ENV = {
     "wpb4": {"MI_CLS_WPB": "4"},       # 4-wave blocks (own hot-region copy or HBM)
     "wpb16": {"MI_CLS_WPB": "16"},     # one 16-wave block per CU sharing the LDS copy
     "nowide": {"MI_CLS_NO_WIDE": "1"},  # candidate lists instead of wide bitmap rows
+    "nocand1": {"MI_CLS_NO_CAND1": "1"},   # no single-candidate engine (wide / lists)
+    "noportmerge": {"MI_CLS_NO_PORTMERGE": "1"},   # separate UDP / TCP port classes
+    "noflat": {"MI_CLS_NO_FLAT": "1"},   # general kernel for flat programs too
 }
 
 
@@ -32,7 +35,8 @@ def both(prog, batch, limits=(255, 8192, 4096), what="", engine="auto"):
     linear scan otherwise, per-lane rounds for CoS trees; the other engines
     force one of the kernel's paths (ENGINE_ENV)."""
     import os
-    keys = ("MI_CLS_NO_BV", "MI_CLS_DIV", "MI_CLS_WPB", "MI_CLS_NO_WIDE")
+    keys = ("MI_CLS_NO_BV", "MI_CLS_DIV", "MI_CLS_WPB", "MI_CLS_NO_WIDE", "MI_CLS_NO_CAND1",
+            "MI_CLS_NO_PORTMERGE", "MI_CLS_NO_FLAT")
     old = {k: os.environ.pop(k, None) for k in keys}
     os.environ.update(ENGINE_ENV[engine])
     try:
@@ -95,7 +99,8 @@ def test_zoo_no_default(built, gpu):
     assert s["discard"] > 0 and s["cos_drop"] > 0
 
 
-@pytest.mark.parametrize("engine", ["auto", "linear", "nodiv", "div", "wpb16", "nowide"])
+@pytest.mark.parametrize("engine", ["auto", "linear", "nodiv", "div", "wpb16", "nowide", "nocand1",
+                                    "noportmerge", "noflat"])
 @pytest.mark.parametrize("seed", range(12))
 def test_random_programs_fuzz(built, gpu, seed, engine):
     rng = np.random.default_rng(1000 + seed)
@@ -108,7 +113,8 @@ def test_random_programs_fuzz(built, gpu, seed, engine):
     both(prog, b, what=f"fuzz seed {seed}", engine=engine)
 
 
-@pytest.mark.parametrize("engine", ["auto", "linear", "nodiv", "wpb4", "wpb16", "nowide"])
+@pytest.mark.parametrize("engine", ["auto", "linear", "nodiv", "wpb4", "wpb16", "nowide", "nocand1",
+                                    "noportmerge", "noflat"])
 @pytest.mark.parametrize("cfg,n", [(1, 10_000), (2, 100_000), (3, 50_000), (4, 50_000),
                                    (5, 20_000)])
 def test_configs_small(built, gpu, cfg, n, engine):
@@ -117,7 +123,7 @@ def test_configs_small(built, gpu, cfg, n, engine):
     assert summary(got)["enq"] > 0
 
 
-@pytest.mark.parametrize("engine", ["auto", "nowide", "div"])
+@pytest.mark.parametrize("engine", ["auto", "nowide", "div", "nocand1", "noflat"])
 @pytest.mark.parametrize("num_rules", [33, 64, 100, 200, 255, 256, 257])
 def test_wide_rule_counts(built, gpu, num_rules, engine):
     """Rule counts around the wide-bitmap engine's word boundaries (33..256

@@ -36,7 +36,7 @@ PY
   done
   i=$((i+1))
 done
-for c in 3 33; do
+for c in ${NOWIDE_CFGS:-}; do
   MI_CLS_NO_WIDE=1 timeout -k 10 200 python bench.py --config $c --steps 20 --warmup 5 --timed-only > $OUT/nowide_c$c.json 2>/dev/null || exit 1
   python -c "import json; d=json.load(open('$OUT/nowide_c$c.json')); print('nowide config $c', d['roofline']['kernel_ms'])"
 done
