@@ -56,7 +56,9 @@ def parse_args():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", type=int, default=3)
-    ap.add_argument("--n", type=int, default=1_000_000, help="packets per GPU")
+    ap.add_argument("--n", "--packets", dest="n", type=int, default=1_000_000,
+                    help="packets per GPU (spell it --packets under torchrun, which would "
+                         "take --n as an abbreviation of its own options)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-extra", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
@@ -329,24 +331,53 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("BENCH_SAME_DEVICE"):   # multi-rank rehearsal on one GPU (tests)
+        local = 0
     dist_on = world > 1
+    backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
     if dist_on:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device(f"cuda:{local}")
 
     from odp_amd import cls, rules as R
-    batch, prog = make_workload(a.config, a.n, rank)
+    # The node's capture is world x n packets; rank r classifies slice r of
+    # it, cut by the product's multi-GPU sharding (mi_cls_shard, the cut
+    # mi_cls_group_classify_host makes: contiguous, balanced by header
+    # bytes) over the capture's frame lengths (IMIX drawn from one node-wide
+    # seed); the slice's packets are generated with the rank's seed.  No
+    # collective on the data path (weak scaling: ~n packets per GPU).
+    n_rank = a.n
+    if world > 1:
+        import numpy as np
+        from odp_amd import pktgen as pg
+        if a.config in (3, 4, 5, 34):
+            node_lens = pg.imix_lens(np.random.default_rng(pg.seed_for(a.config) ^ 0x5EED),
+                                     a.n * world)
+        else:
+            node_lens = np.full(a.n * world, 60)
+        bnd = cls.shard(node_lens.astype(np.uint16), world)
+        n_rank = int(bnd[rank + 1] - bnd[rank])
+    batch, prog = make_workload(a.config, n_rank, rank)
     c = cls.Classifier(gpu=local)
     c.apply(prog)
 
     wall, kms, t_out = time_device(c, batch, dev, a.steps, a.warmup, dist_on, a.rotate,
                                    a.streams)
+    red_dev = dev if backend == "nccl" else torch.device("cpu")   # where reductions run
     if dist_on:
-        t = torch.tensor([wall], dtype=torch.float64, device=dev)
+        t = torch.tensor([wall], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall = float(t.item())
-    total_pkts = batch.n * world * a.steps
+    if dist_on:
+        tn = torch.tensor([batch.n], dtype=torch.float64, device=red_dev)
+        dist.all_reduce(tn, op=dist.ReduceOp.SUM)
+        total_pkts = int(tn.item()) * a.steps
+    else:
+        total_pkts = batch.n * a.steps
     value = total_pkts / wall / 1e6
     bytes_launch = batch.header_bytes()
     achieved = bytes_launch / (kms * 1e-3) / 1e9
@@ -368,6 +399,7 @@ def main():
             "dtype": "u8",
             "data": "synthetic",
             "config": {"workload": WORKLOAD[a.config], "packets_per_gpu": batch.n,
+                       "packets_total": total_pkts // a.steps,
                        "rules": R.rule_count(prog), "cos": R.cos_count(prog),
                        "frame_bytes": "60 (64 B on the wire)" if a.config in (2, 33)
                        else "IMIX 60/566/1514 7:4:1" if a.config == 3 else "mixed",
@@ -380,11 +412,12 @@ def main():
                          "bytes_per_launch": bytes_launch,
                          "traffic_source": (pmc or {}).get("source")},
         }
+        if not a.no_parity and not a.timed_only:
+            # this rank's records, every one bit-exact vs the oracle
+            line["parity_vs_oracle"] = oracle_parity(prog, batch, out)
         if world == 1 and not a.timed_only:
             if R.rule_count(prog) >= 256:
                 line["compute"] = compute_roof(prog, batch, kms, pmc)
-            if not a.no_parity:
-                line["parity_vs_oracle"] = oracle_parity(prog, batch, out)
             w2, _, _ = time_device(c, batch, dev, a.steps, a.warmup, rotate=a.rotate, streams=2)
             line["pipelined"] = {"streams": 2, "mpkts_per_s": round(batch.n * a.steps / w2 / 1e6, 2),
                                  "ms_per_step": round(w2 / a.steps * 1e3, 5)}

@@ -195,6 +195,40 @@ int mi_cls_classify_host(mi_cls_ctx_t *ctx, const uint8_t *pkts_host, size_t byt
 			 const uint32_t *off_host, const uint16_t *len_host, uint32_t n,
 			 mi_cls_result_t *out_host);
 
+/* ------------------------------------------------------------------------
+ * Multi-GPU: one host batch over several devices.
+ * The batch shards with no exchange step: mi_cls_shard cuts it into
+ * contiguous slices balanced by the bytes the kernel reads per packet
+ * (min(len,128) + 6 B descriptor + 16 B record); each slice is staged,
+ * classified and copied back on its own context and stream, all devices in
+ * flight at once; the records land at their packets' positions in `out`, so
+ * the result is the single-device result and per-queue arrival order is the
+ * one the reference's _odp_cls_enq runs see
+ * (platform/linux-generic/include/odp_classification_internal.h:208-236).
+ * Replaces running the per-burst loopback_recv (pktio/loop.c:253-384) once
+ * per device.
+ * ---------------------------------------------------------------------- */
+typedef struct mi_cls_group mi_cls_group_t;
+
+/* begin[0..nshards]: slice k is packets [begin[k], begin[k+1]). */
+int mi_cls_shard(const uint16_t *len, uint32_t n, uint32_t nshards, uint32_t *begin);
+
+/* One context per entry of devices[] (an id may repeat: several contexts on
+ * one device). */
+int mi_cls_group_create(const int *devices, uint32_t n, mi_cls_group_t **group);
+int mi_cls_group_destroy(mi_cls_group_t *group);
+uint32_t mi_cls_group_size(const mi_cls_group_t *group);
+mi_cls_ctx_t *mi_cls_group_ctx(mi_cls_group_t *group, uint32_t i);
+/* The rule table replicated to every device (synchronous). */
+int mi_cls_group_rules_load(mi_cls_group_t *group, const void *tbl, size_t bytes);
+int mi_cls_group_pktin_opt_set(mi_cls_group_t *group, uint64_t opt);
+/* As mi_cls_classify_host, sharded over the group's devices; returns when
+ * every record is in out_host.  Pinned input (mi_cls_host_alloc) lets the
+ * devices' copies overlap. */
+int mi_cls_group_classify_host(mi_cls_group_t *group, const uint8_t *pkts_host, size_t bytes,
+			       const uint32_t *off_host, const uint16_t *len_host, uint32_t n,
+			       mi_cls_result_t *out_host);
+
 /* pktin parse options for the following classify calls on this context:
  * odp_pktin_config_opt_t.all_bits (include/odp_rt.h; reference
  * include/odp/api/spec/packet_io.h odp_pktin_config_opt_t).  Bits 2-5

@@ -270,6 +270,9 @@ void odp_amd_cls_reset(void);
  * of a pktio entry (odp_classification_datamodel.h:176-181) plus its device
  * context.  odp_pktio_open() of the ODP runtime layer creates these. */
 odp_pktio_t odp_amd_cls_pktio_create(int gpu);
+/* Classifier endpoint whose host bursts are sharded over gpus[0..n) (n <= 16;
+ * ids may repeat); the runtime opens pktios this way when ODP_AMD_GPUS is set. */
+odp_pktio_t odp_amd_cls_pktio_create_multi(const int *gpus, int n);
 int odp_amd_cls_pktio_destroy(odp_pktio_t pktio);
 
 /* Snapshot ("compile") the current tables into the mi_cls.h blob format.

@@ -130,6 +130,9 @@ def _load():
         "odp_amd_cls_limits_set": (i32, [u32, u32, u32]),
         "odp_amd_cls_reset": (None, []),
         "odp_amd_cls_pktio_create": (vp, [i32]),
+        "odp_amd_cls_pktio_create_multi": (vp, [C.POINTER(i32), i32]),
+        "odp_amd_cls_classify_host": (i32, [vp, vp, C.c_size_t, vp, vp, u32, vp, i32]),
+        "mi_cls_shard": (i32, [vp, u32, u32, vp]),
         "odp_amd_cls_pktio_destroy": (i32, [vp]),
         "odp_amd_cls_compile": (C.c_long, [vp, vp, C.c_size_t]),
         "odp_amd_cls_classify": (i32, [vp, vp, vp, vp, u32, vp, vp]),
@@ -154,6 +157,17 @@ def _load():
 _lib = None
 
 
+def shard(lens: np.ndarray, nshards: int) -> np.ndarray:
+    """mi_cls_shard: begin[0..nshards] of contiguous slices balanced by
+    header-window bytes (the product's multi-GPU cut; host only)."""
+    ln = np.ascontiguousarray(lens, dtype=np.uint16)
+    begin = np.zeros(nshards + 1, dtype=np.uint32)
+    rc = lib().mi_cls_shard(ln.ctypes.data, int(ln.shape[0]), nshards, begin.ctypes.data)
+    if rc:
+        raise RuntimeError(f"mi_cls_shard: {rc}")
+    return begin
+
+
 def lib():
     global _lib
     if _lib is None:
@@ -170,13 +184,19 @@ class Classifier:
     through the ODP classification API.  ``apply(program)`` replays a rule
     program (odp_amd.rules) with odp_cls_* calls."""
 
-    def __init__(self, gpu: int = 0, limits=(255, 8192, 4096)):
+    def __init__(self, gpu: int = 0, limits=(255, 8192, 4096), gpus=None):
+        """gpus: a list of device ids -- host batches (classify_host) are then
+        sharded over them (mi_cls_group_classify_host)."""
         L = lib()
         L.odp_amd_cls_reset()
         if limits is not None:
             assert L.odp_amd_cls_limits_set(*limits) == 0
         self.L = L
-        self.pktio = L.odp_amd_cls_pktio_create(gpu)
+        if gpus:
+            arr = (C.c_int * len(gpus))(*gpus)
+            self.pktio = L.odp_amd_cls_pktio_create_multi(arr, len(gpus))
+        else:
+            self.pktio = L.odp_amd_cls_pktio_create(gpu)
         if not self.pktio:
             raise RuntimeError("odp_amd_cls_pktio_create failed")
         self.cos = []
@@ -298,6 +318,21 @@ class Classifier:
         torch.cuda.synchronize(dev)
         out = t_out.cpu().numpy().view(np.uint8).reshape(-1)[: 16 * batch.n]
         return out.view(R.RESULT_DTYPE).copy()
+
+    def classify_host(self, batch):
+        """The pktio receive-path entry (odp_amd_cls_classify_host): the
+        batch from host memory, staged, classified (sharded over the
+        pktio's GPUs when it has several) and the records copied back."""
+        out = np.zeros(max(1, batch.n), dtype=R.RESULT_DTYPE)
+        buf = np.ascontiguousarray(batch.buf)
+        off = np.ascontiguousarray(batch.off, dtype=np.uint32)
+        ln = np.ascontiguousarray(batch.len, dtype=np.uint16)
+        rc = self.L.odp_amd_cls_classify_host(self.pktio, buf.ctypes.data, buf.nbytes,
+                                              off.ctypes.data, ln.ctypes.data, batch.n,
+                                              out.ctypes.data, 0)
+        if rc != 0:
+            raise RuntimeError(f"odp_amd_cls_classify_host: {rc}")
+        return out[: batch.n]
 
     def cos_stats_packets(self, cos_handle):
         s = CosStats()

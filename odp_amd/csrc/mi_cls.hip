@@ -25,6 +25,8 @@ struct mi_cls_ctx {
 	int num_cu;
 	// host-batch staging (mi_cls_classify_host)
 	hipStream_t stream;
+	uint32_t *h_off;         // pinned: rebased descriptors of a slice
+	mi_cls_result_t *h_out;  // pinned: records of a slice (multi-GPU)
 	uint8_t *d_pk;
 	size_t pk_cap;
 	uint32_t *d_off;
@@ -95,6 +97,8 @@ extern "C" int mi_cls_ctx_destroy(mi_cls_ctx_t *c)
 	(void)hipFree(c->d_off);
 	(void)hipFree(c->d_len);
 	(void)hipFree(c->d_out);
+	(void)hipHostFree(c->h_off);
+	(void)hipHostFree(c->h_out);
 	free(c);
 	return 0;
 }
@@ -1049,6 +1053,66 @@ extern "C" int mi_cls_classify(mi_cls_ctx_t *c, const uint8_t *pkts, const uint3
 	return 0;
 }
 
+// Stage frames [lo, hi) of a host batch (descriptors rebased by lo) through
+// the context's device buffers on its own stream and launch the kernel; the
+// records go to `out` (any host memory) or, when out is NULL, to the
+// context's pinned record buffer h_out (multi-GPU: no host wait per device).
+// Nothing is waited for here.
+static int host_launch(mi_cls_ctx_t *c, const uint8_t *pkts, size_t lo, size_t hi,
+		       const uint32_t *off, const uint16_t *len, uint32_t n, mi_cls_result_t *out)
+{
+	HIP_OK(hipSetDevice(c->device));
+	if (!c->stream)
+		HIP_OK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+	const size_t bytes = hi - lo;
+	const size_t need = bytes + 64;
+	if (need > c->pk_cap) {
+		(void)hipFree(c->d_pk);
+		c->d_pk = nullptr;
+		size_t cap = need < (1u << 20) ? (1u << 20) : need + need / 2;
+		if (hipMalloc((void **)&c->d_pk, cap) != hipSuccess)
+			return c->pk_cap = 0, -ENOMEM;
+		HIP_OK(hipMemset(c->d_pk, 0, cap));
+		c->pk_cap = cap;
+	}
+	if (n > c->n_cap) {
+		(void)hipFree(c->d_off);
+		(void)hipFree(c->d_len);
+		(void)hipFree(c->d_out);
+		(void)hipHostFree(c->h_off);
+		(void)hipHostFree(c->h_out);
+		c->d_off = nullptr;
+		c->d_len = nullptr;
+		c->d_out = nullptr;
+		c->h_off = nullptr;
+		c->h_out = nullptr;
+		uint32_t cap = n < 4096u ? 4096u : n + n / 2;
+		if (hipMalloc((void **)&c->d_off, cap * sizeof(uint32_t)) != hipSuccess ||
+		    hipMalloc((void **)&c->d_len, cap * sizeof(uint16_t)) != hipSuccess ||
+		    hipMalloc((void **)&c->d_out, cap * sizeof(mi_cls_result_t)) != hipSuccess ||
+		    hipHostMalloc((void **)&c->h_off, cap * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
+		    hipHostMalloc((void **)&c->h_out, cap * sizeof(mi_cls_result_t), hipHostMallocDefault) != hipSuccess)
+			return c->n_cap = 0, -ENOMEM;
+		c->n_cap = cap;
+	}
+	hipStream_t s = c->stream;
+	const uint32_t *doff = off;
+	if (lo) {
+		for (uint32_t i = 0; i < n; ++i)
+			c->h_off[i] = off[i] - (uint32_t)lo;
+		doff = c->h_off;
+	}
+	HIP_OK(hipMemcpyAsync(c->d_pk, pkts + lo, bytes, hipMemcpyHostToDevice, s));
+	HIP_OK(hipMemcpyAsync(c->d_off, doff, n * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+	HIP_OK(hipMemcpyAsync(c->d_len, len, n * sizeof(uint16_t), hipMemcpyHostToDevice, s));
+	int rc = mi_cls_classify(c, c->d_pk, c->d_off, c->d_len, n, c->d_out, s);
+	if (rc)
+		return rc;
+	HIP_OK(hipMemcpyAsync(out ? out : c->h_out, c->d_out, n * sizeof(mi_cls_result_t),
+			      hipMemcpyDeviceToHost, s));
+	return 0;
+}
+
 // Host-memory batch: stage through device buffers owned by the context on its
 // own stream (grown geometrically, kept across calls), classify, copy back.
 extern "C" int mi_cls_classify_host(mi_cls_ctx_t *c, const uint8_t *pkts, size_t bytes,
@@ -1066,43 +1130,169 @@ extern "C" int mi_cls_classify_host(mi_cls_ctx_t *c, const uint8_t *pkts, size_t
 	for (uint32_t i = 0; i < n; ++i)
 		if ((size_t)off[i] + len[i] > bytes)
 			return -EINVAL;
-	HIP_OK(hipSetDevice(c->device));
-	if (!c->stream)
-		HIP_OK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-	const size_t need = bytes + 64;
-	if (need > c->pk_cap) {
-		(void)hipFree(c->d_pk);
-		c->d_pk = nullptr;
-		size_t cap = need < (1u << 20) ? (1u << 20) : need + need / 2;
-		if (hipMalloc((void **)&c->d_pk, cap) != hipSuccess)
-			return c->pk_cap = 0, -ENOMEM;
-		HIP_OK(hipMemset(c->d_pk, 0, cap));
-		c->pk_cap = cap;
-	}
-	if (n > c->n_cap) {
-		(void)hipFree(c->d_off);
-		(void)hipFree(c->d_len);
-		(void)hipFree(c->d_out);
-		c->d_off = nullptr;
-		c->d_len = nullptr;
-		c->d_out = nullptr;
-		uint32_t cap = n < 4096u ? 4096u : n + n / 2;
-		if (hipMalloc((void **)&c->d_off, cap * sizeof(uint32_t)) != hipSuccess ||
-		    hipMalloc((void **)&c->d_len, cap * sizeof(uint16_t)) != hipSuccess ||
-		    hipMalloc((void **)&c->d_out, cap * sizeof(mi_cls_result_t)) != hipSuccess)
-			return c->n_cap = 0, -ENOMEM;
-		c->n_cap = cap;
-	}
-	hipStream_t s = c->stream;
-	HIP_OK(hipMemcpyAsync(c->d_pk, pkts, bytes, hipMemcpyHostToDevice, s));
-	HIP_OK(hipMemcpyAsync(c->d_off, off, n * sizeof(uint32_t), hipMemcpyHostToDevice, s));
-	HIP_OK(hipMemcpyAsync(c->d_len, len, n * sizeof(uint16_t), hipMemcpyHostToDevice, s));
-	int rc = mi_cls_classify(c, c->d_pk, c->d_off, c->d_len, n, c->d_out, s);
+	int rc = host_launch(c, pkts, 0, bytes, off, len, n, out);
 	if (rc)
 		return rc;
-	HIP_OK(hipMemcpyAsync(out, c->d_out, n * sizeof(mi_cls_result_t), hipMemcpyDeviceToHost, s));
-	HIP_OK(hipStreamSynchronize(s));
+	HIP_OK(hipStreamSynchronize(c->stream));
 	return 0;
+}
+
+// ---------------------------------------------------------------- multi-GPU
+// the batch shards with no exchange step.  Contiguous
+// slices balanced by the bytes the kernel reads per packet (min(len,128) +
+// 6 B descriptor + 16 B record), one per device; concatenating the slices'
+// records in device order is the single-device result, so per-queue arrival
+// order is what the reference's _odp_cls_enq runs see
+// (odp_classification_internal.h:208-236).
+extern "C" int mi_cls_shard(const uint16_t *len, uint32_t n, uint32_t nshards, uint32_t *begin)
+{
+	if (!begin || nshards == 0 || (n && !len))
+		return -EINVAL;
+	uint64_t total = 0;
+	for (uint32_t i = 0; i < n; ++i)
+		total += (uint64_t)(len[i] < 128u ? len[i] : 128u) + 22u;
+	begin[0] = 0;
+	uint64_t cum = 0;
+	uint32_t i = 0;
+	for (uint32_t r = 1; r < nshards; ++r) {
+		// first packet index whose running total reaches r/nshards of the
+		// whole; the cut follows it
+		while (i < n && (cum + (uint64_t)(len[i] < 128u ? len[i] : 128u) + 22u) * nshards <
+				       total * r) {
+			cum += (uint64_t)(len[i] < 128u ? len[i] : 128u) + 22u;
+			++i;
+		}
+		begin[r] = i < n ? i + 1u : n;
+		if (begin[r] < begin[r - 1])
+			begin[r] = begin[r - 1];
+	}
+	begin[nshards] = n;
+	for (uint32_t r = 1; r < nshards; ++r)
+		if (begin[r] > n)
+			begin[r] = n;
+	return 0;
+}
+
+#define MI_GROUP_MAX 64
+struct mi_cls_group {
+	uint32_t n;
+	mi_cls_ctx_t *ctx[MI_GROUP_MAX];
+	uint32_t *begin;          // nshards + 1
+};
+
+extern "C" int mi_cls_group_create(const int *devices, uint32_t n, mi_cls_group_t **out)
+{
+	if (!devices || !out || n == 0 || n > MI_GROUP_MAX)
+		return -EINVAL;
+	mi_cls_group_t *g = (mi_cls_group_t *)calloc(1, sizeof(*g));
+	if (!g)
+		return -ENOMEM;
+	g->begin = (uint32_t *)calloc(n + 1, sizeof(uint32_t));
+	if (!g->begin) {
+		free(g);
+		return -ENOMEM;
+	}
+	for (uint32_t i = 0; i < n; ++i) {
+		int rc = mi_cls_ctx_create(devices[i], &g->ctx[i]);
+		if (rc) {
+			g->n = i;
+			mi_cls_group_destroy(g);
+			return rc;
+		}
+	}
+	g->n = n;
+	*out = g;
+	return 0;
+}
+
+extern "C" int mi_cls_group_destroy(mi_cls_group_t *g)
+{
+	if (!g)
+		return -EINVAL;
+	for (uint32_t i = 0; i < g->n; ++i)
+		mi_cls_ctx_destroy(g->ctx[i]);
+	free(g->begin);
+	free(g);
+	return 0;
+}
+
+extern "C" uint32_t mi_cls_group_size(const mi_cls_group_t *g)
+{
+	return g ? g->n : 0u;
+}
+
+extern "C" mi_cls_ctx_t *mi_cls_group_ctx(mi_cls_group_t *g, uint32_t i)
+{
+	return g && i < g->n ? g->ctx[i] : nullptr;
+}
+
+extern "C" int mi_cls_group_rules_load(mi_cls_group_t *g, const void *tbl, size_t bytes)
+{
+	if (!g)
+		return -EINVAL;
+	for (uint32_t i = 0; i < g->n; ++i) {
+		int rc = mi_cls_rules_load(g->ctx[i], tbl, bytes, nullptr);
+		if (rc)
+			return rc;
+	}
+	return 0;
+}
+
+extern "C" int mi_cls_group_pktin_opt_set(mi_cls_group_t *g, uint64_t opt)
+{
+	if (!g)
+		return -EINVAL;
+	for (uint32_t i = 0; i < g->n; ++i)
+		mi_cls_pktin_opt_set(g->ctx[i], opt);
+	return 0;
+}
+
+extern "C" int mi_cls_group_classify_host(mi_cls_group_t *g, const uint8_t *pkts, size_t bytes,
+					  const uint32_t *off, const uint16_t *len, uint32_t n,
+					  mi_cls_result_t *out)
+{
+	if (!g)
+		return -EINVAL;
+	if (n == 0)
+		return 0;
+	if (!pkts || !off || !len || !out)
+		return -EINVAL;
+	for (uint32_t k = 0; k < g->n; ++k)
+		if (!g->ctx[k]->loaded)
+			return -EINVAL;
+	for (uint32_t i = 0; i < n; ++i)
+		if ((size_t)off[i] + len[i] > bytes)
+			return -EINVAL;
+	int rc = mi_cls_shard(len, n, g->n, g->begin);
+	if (rc)
+		return rc;
+	// every device's slice in flight before any wait
+	int first_err = 0;
+	for (uint32_t k = 0; k < g->n && !first_err; ++k) {
+		const uint32_t b = g->begin[k], e = g->begin[k + 1];
+		if (b == e)
+			continue;
+		size_t lo = off[b], hi = 0;
+		for (uint32_t i = b; i < e; ++i) {
+			lo = off[i] < lo ? off[i] : lo;
+			hi = (size_t)off[i] + len[i] > hi ? (size_t)off[i] + len[i] : hi;
+		}
+		lo &= ~(size_t)15;   // keep the slice's 16-B alignment
+		first_err = host_launch(g->ctx[k], pkts, lo, hi, off + b, len + b, e - b, nullptr);
+	}
+	for (uint32_t k = 0; k < g->n; ++k) {
+		const uint32_t b = g->begin[k], e = g->begin[k + 1];
+		if (b == e || !g->ctx[k]->stream)
+			continue;
+		if (hipSetDevice(g->ctx[k]->device) != hipSuccess ||
+		    hipStreamSynchronize(g->ctx[k]->stream) != hipSuccess) {
+			first_err = first_err ? first_err : -EIO;
+			continue;
+		}
+		if (!first_err)
+			memcpy(out + b, g->ctx[k]->h_out, (size_t)(e - b) * sizeof(mi_cls_result_t));
+	}
+	return first_err;
 }
 
 // pktin options for the following classify calls: odp_pktin_config_opt_t

@@ -993,16 +993,30 @@ __device__ __forceinline__ uint32_t bv_bucket(uint32_t x, uint32_t m, uint32_t n
 // Word readers of a classification block: wave-uniform blocks are read with
 // scalar loads from HBM (DescU), per-lane blocks from the hot region (LDS or
 // HBM, DescL).
+// A wave-uniform 16-word descriptor (block header, class record) held in
+// SGPRs: one s_load_dwordx16, one wait, instead of a scalar load and wait
+// per word on use.
+typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
+struct DescV {
+	u32x16 v;
+	__device__ __forceinline__ uint32_t operator()(uint32_t i) const { return v[i]; }
+};
 struct DescU {
 	cword_t p;
 	__device__ __forceinline__ uint32_t operator()(uint32_t i) const { return p[i]; }
 	__device__ __forceinline__ DescU at(uint32_t o) const { return DescU{ p + o }; }
+	// 16 words at o, loaded at once (o: compile-time word offset)
+	__device__ __forceinline__ DescV vec(uint32_t o) const
+	{
+		return DescV{ *(const __attribute__((address_space(4))) u32x16 *)(p + o) };
+	}
 };
 template <typename T> struct DescL {
 	T p;
 	uint32_t b;
 	__device__ __forceinline__ uint32_t operator()(uint32_t i) const { return p[b + i]; }
 	__device__ __forceinline__ DescL at(uint32_t o) const { return DescL{ p, b + o }; }
+	__device__ __forceinline__ DescL vec(uint32_t o) const { return at(o); }
 };
 
 // Key of a packet for one class: the masked field the class's terms
@@ -1098,7 +1112,8 @@ __device__ __forceinline__ void bv_eval(const D &blk, T H, bool act, const Pkt &
 					const Fields &x, uint32_t &hit, uint32_t &nxt, uint32_t &nmark,
 					uint32_t &nleaf)
 {
-	const uint32_t mode = FM >= 0 ? (uint32_t)FM : blk(0), ncls = blk(1), res = blk(2);
+	const auto hb = blk.vec(0);   // the block header (words 0-7)
+	const uint32_t mode = FM >= 0 ? (uint32_t)FM : hb(0), ncls = hb(1), res = hb(2);
 	uint32_t first = BV_NONE;
 	if (mode == 0u) {
 		// direct: one class, the slot holds 1 + the first live rule of its
@@ -1110,11 +1125,11 @@ __device__ __forceinline__ void bv_eval(const D &blk, T H, bool act, const Pkt &
 		first = val != 0u ? (val == BV_EMPTY ? BV_NONE : val - 1u) : cr(2);
 	} else if (mode == 2u) {
 		// bitmap: AND of the classes' 32-bit rows and the alive row
-		uint32_t acc = blk(4);
+		uint32_t acc = hb(4);
 #pragma unroll
 		for (uint32_t kc = 0; kc < BV_MAX_CLS; ++kc) {
 			if (kc < ncls) {
-				const D cr = blk.at(8u + BV_CLS_WORDS * kc);
+				const auto cr = blk.vec(8u + BV_CLS_WORDS * kc);
 				uint32_t key[4];
 				const bool present = bv_key(cr, k, p, x, key);
 				const uint32_t val = bv_lookup(cr, H, key, act && present);
@@ -1130,7 +1145,7 @@ __device__ __forceinline__ void bv_eval(const D &blk, T H, bool act, const Pkt &
 		// rows are split in halves: words 0-3 at the value, words 4-7
 		// `half` words further (consecutive rows are then 16 B apart, so the
 		// 16-lane groups of a 16-B LDS read spread over all 64 banks)
-		const uint32_t ar = blk(4), half = blk(7);
+		const uint32_t ar = hb(4), half = hb(7);
 		uint32_t acc[BV_WIDE_WORDS];
 #pragma unroll
 		for (uint32_t i = 0; i < BV_WIDE_WORDS; ++i)
@@ -1138,7 +1153,7 @@ __device__ __forceinline__ void bv_eval(const D &blk, T H, bool act, const Pkt &
 #pragma unroll
 		for (uint32_t kc = 0; kc < BV_MAX_CLS; ++kc) {
 			if (kc < ncls) {
-				const D cr = blk.at(8u + BV_CLS_WORDS * kc);
+				const auto cr = blk.vec(8u + BV_CLS_WORDS * kc);
 				uint32_t key[4];
 				const bool present = bv_key(cr, k, p, x, key);
 				const uint32_t val = bv_lookup(cr, H, key, act && present);
@@ -1160,15 +1175,15 @@ __device__ __forceinline__ void bv_eval(const D &blk, T H, bool act, const Pkt &
 		// ids); each hit names the one rule filed under the packet's key,
 		// whose record is checked against the packet's keys of every class
 		// it constrains; the smallest holding candidate wins
-		const uint32_t rec0 = blk(4), rw = blk(5), lk = blk(6), pm = blk(7);
+		const uint32_t rec0 = hb(4), rw = hb(5), lk = hb(6), pm = hb(7);
 		uint32_t cmpv[BV_MAX_CLS], cand[BV_MAX_CLS], prm = 0;
-		first = blk(3);   // the first rule without a classified term
+		first = hb(3);   // the first rule without a classified term
 #pragma unroll
 		for (uint32_t kc = 0; kc < BV_MAX_CLS; ++kc) {
 			cmpv[kc] = 0u;
 			cand[kc] = 0u;
 			if (kc < ncls) {
-				const D cr = blk.at(8u + BV_CLS_WORDS * kc);
+				const auto cr = blk.vec(8u + BV_CLS_WORDS * kc);
 				uint32_t key[4];
 				const bool present = bv_key(cr, k, p, x, key);
 				prm |= present ? 1u << kc : 0u;
@@ -1209,21 +1224,21 @@ __device__ __forceinline__ void bv_eval(const D &blk, T H, bool act, const Pkt &
 		}
 	} else {
 		// candidate: key id per class, then the candidates' records
-		const uint32_t rec0 = blk(4), rw = blk(5);
+		const uint32_t rec0 = hb(4), rw = hb(5);
 		uint32_t v[BV_MAX_CLS], lb[BV_MAX_CLS];
 #pragma unroll
 		for (uint32_t kc = 0; kc < BV_MAX_CLS; ++kc) {
 			v[kc] = 0u;
 			lb[kc] = 0u;
 			if (kc < ncls) {
-				const D cr = blk.at(8u + BV_CLS_WORDS * kc);
+				const auto cr = blk.vec(8u + BV_CLS_WORDS * kc);
 				uint32_t key[4];
 				const bool present = bv_key(cr, k, p, x, key);
 				v[kc] = bv_lookup(cr, H, key, act && present);
 				lb[kc] = cr(13);
 			}
 		}
-		first = blk(3);   // the first rule without a classified term
+		first = hb(3);   // the first rule without a classified term
 #pragma unroll
 		for (uint32_t kc = 0; kc < BV_MAX_CLS; ++kc) {
 			if (kc < ncls) {

@@ -78,8 +78,13 @@ typedef struct {
 	int default_cos;       /* slot, -1 none */
 	int error_cos;
 	uint32_t headroom;
-	mi_cls_ctx_t *ctx;
+	mi_cls_ctx_t *ctx;       /* device 0 of the pktio (the group's first context) */
 	mi_cls_ctx_t *pctx;      /* parse-only context (empty table) */
+	/* multi-GPU receive (odp_amd_cls_pktio_create_multi): host bursts are
+	 * sharded over these devices (mi_cls_group_classify_host) */
+	mi_cls_group_t *grp;
+	int ngpu;
+	int gpus[16];
 	uint64_t compiled_gen;
 	void *blob;
 	size_t blob_cap;
@@ -720,13 +725,31 @@ odp_pktio_t odp_amd_cls_pktio_create(int gpu)
 	return ODP_PKTIO_INVALID;
 }
 
+/* A classifier endpoint whose host bursts are sharded over several GPUs
+ * (SURVEY.md §8(e)); gpus[0] also serves the device-pointer entry. */
+odp_pktio_t odp_amd_cls_pktio_create_multi(const int *gpus, int n)
+{
+	if (!gpus || n < 1 || n > 16)
+		return ODP_PKTIO_INVALID;
+	odp_pktio_t h = odp_amd_cls_pktio_create(gpus[0]);
+	pktio_t *e = get_pktio(h);
+
+	if (!e)
+		return ODP_PKTIO_INVALID;
+	e->ngpu = n;
+	memcpy(e->gpus, gpus, (size_t)n * sizeof(int));
+	return h;
+}
+
 int odp_amd_cls_pktio_destroy(odp_pktio_t h)
 {
 	pktio_t *e = get_pktio(h);
 
 	if (!e)
 		return -1;
-	if (e->ctx)
+	if (e->grp)
+		mi_cls_group_destroy(e->grp);   /* owns e->ctx */
+	else if (e->ctx)
 		mi_cls_ctx_destroy(e->ctx);
 	if (e->pctx)
 		mi_cls_ctx_destroy(e->pctx);
@@ -1022,8 +1045,14 @@ int odp_cls_cos_stats(odp_cos_t h, odp_cls_cos_stats_t *stats)
 
 		if (!e->used || !e->ctx)
 			continue;
-		if (mi_cls_stats_read(e->ctx, buf, 256) == 0)
-			stats->packets += buf[c->index];
+		uint32_t nc = e->grp ? mi_cls_group_size(e->grp) : 1u;
+
+		for (uint32_t k = 0; k < nc; k++) {
+			mi_cls_ctx_t *x = e->grp ? mi_cls_group_ctx(e->grp, k) : e->ctx;
+
+			if (mi_cls_stats_read(x, buf, 256) == 0)
+				stats->packets += buf[c->index];
+		}
 	}
 	return 0;
 }
@@ -1177,7 +1206,17 @@ odp_pool_t odp_amd_cls_pool_of(uint32_t cos_index)
 
 static int ensure_ctx(pktio_t *e)
 {
-	return e->ctx ? 0 : mi_cls_ctx_create(e->gpu, &e->ctx);
+	if (e->ctx)
+		return 0;
+	if (e->ngpu > 1) {
+		int rc = mi_cls_group_create(e->gpus, (uint32_t)e->ngpu, &e->grp);
+
+		if (rc)
+			return rc;
+		e->ctx = mi_cls_group_ctx(e->grp, 0);
+		return 0;
+	}
+	return mi_cls_ctx_create(e->gpu, &e->ctx);
 }
 
 /* snapshot + upload when the control plane changed (caller: data path) */
@@ -1204,7 +1243,8 @@ static int sync_rules(pktio_t *e, void *stream)
 	}
 	compile_locked(e, e->blob, e->blob_cap);
 	pthread_mutex_unlock(&G.lock);
-	int rc = mi_cls_rules_load(e->ctx, e->blob, (size_t)need, stream);
+	int rc = e->grp ? mi_cls_group_rules_load(e->grp, e->blob, (size_t)need)
+			: mi_cls_rules_load(e->ctx, e->blob, (size_t)need, stream);
 
 	if (rc)
 		return rc;
@@ -1212,7 +1252,12 @@ static int sync_rules(pktio_t *e, void *stream)
 
 	for (int i = 0; i < 8; i++)
 		any |= e->stats_mask[i] != 0;
-	mi_cls_stats_enable(e->ctx, any ? e->stats_mask : NULL);
+	if (e->grp) {
+		for (uint32_t k = 0; k < mi_cls_group_size(e->grp); k++)
+			mi_cls_stats_enable(mi_cls_group_ctx(e->grp, k), any ? e->stats_mask : NULL);
+	} else {
+		mi_cls_stats_enable(e->ctx, any ? e->stats_mask : NULL);
+	}
 	e->compiled_gen = gen;
 	return 0;
 }
@@ -1268,6 +1313,11 @@ int odp_amd_cls_classify_host(odp_pktio_t h, const uint8_t *pkts, size_t bytes,
 	rc = sync_rules(e, NULL);
 	if (rc)
 		return rc;
+	if (e->grp) {
+		mi_cls_group_pktin_opt_set(e->grp, e->pktin_opt);
+		return mi_cls_group_classify_host(e->grp, pkts, bytes, off, len, n,
+						  (mi_cls_result_t *)out);
+	}
 	mi_cls_pktin_opt_set(e->ctx, e->pktin_opt);
 	return mi_cls_classify_host(e->ctx, pkts, bytes, off, len, n, (mi_cls_result_t *)out);
 }

@@ -428,8 +428,23 @@ odp_pktio_t odp_pktio_open(const char *name, odp_pool_t pool, const odp_pktio_pa
 		RT_ERR("pktio %s already open\n", name);
 		return ODP_PKTIO_INVALID;
 	}
-	/* the classifier endpoint (classifier_t + device context) gives the handle */
-	odp_pktio_t h = odp_amd_cls_pktio_create((int)rt_gpu_index());
+	/* the classifier endpoint (classifier_t + device context) gives the
+	 * handle; ODP_AMD_GPUS="0,1,..." shards each receive burst over several
+	 * GPUs (mi_cls_group_classify_host), otherwise ODP_AMD_GPU picks one */
+	int gpus[16], ngpu = 0;
+	const char *ge = getenv("ODP_AMD_GPUS");
+
+	while (ge && *ge && ngpu < 16) {
+		char *end;
+		long v = strtol(ge, &end, 10);
+
+		if (end == ge)
+			break;
+		gpus[ngpu++] = (int)v;
+		ge = *end == ',' ? end + 1 : end;
+	}
+	odp_pktio_t h = ngpu > 1 ? odp_amd_cls_pktio_create_multi(gpus, ngpu)
+				 : odp_amd_cls_pktio_create(ngpu == 1 ? gpus[0] : (int)rt_gpu_index());
 
 	if (h == ODP_PKTIO_INVALID)
 		return h;

@@ -16,7 +16,19 @@ import numpy as np
 
 def shard_bounds(lens: np.ndarray, world: int) -> list[tuple[int, int]]:
     """Contiguous [begin, end) slices, one per rank, balanced by the bytes the
-    kernel reads per packet (min(len,128) + descriptor + record)."""
+    kernel reads per packet (min(len,128) + descriptor + record).  This is
+    the product's cut (mi_cls_shard in libmi_cls.so, the one
+    mi_cls_group_classify_host uses), so a multi-process run and a
+    multi-GPU pktio shard identically."""
+    from .cls import shard
+    if world <= 1:
+        return [(0, int(lens.shape[0]))]
+    b = shard(lens, world)
+    return [(int(b[r]), int(b[r + 1])) for r in range(world)]
+
+
+def shard_bounds_reference(lens: np.ndarray, world: int) -> list[tuple[int, int]]:
+    """numpy restatement of mi_cls_shard (tests cross-check the two)."""
     n = int(lens.shape[0])
     if world <= 1 or n == 0:
         return [(0, n)] + [(n, n)] * max(0, world - 1)

@@ -1,8 +1,12 @@
 """World-size-2 rehearsal of the multi-GPU path on CPU (gloo): each rank
-classifies its own contiguous shard (here with the CPU oracle standing in for
-the per-GPU kernel, which needs a device), results gathered in rank order
-must equal the single-process run, and the bench's max-over-ranks timing
-reduction is exercised with the same collective calls the GPU run makes."""
+takes its contiguous shard with the product's cut (mi_cls_shard in
+libmi_cls.so, the one mi_cls_group_classify_host and bench.py use) and
+classifies it (here with the CPU oracle standing in for the per-GPU kernel,
+which needs a device); results gathered in rank order must equal the
+single-process run, and the bench's max-over-ranks timing reduction is
+exercised with the same collective calls the GPU run makes.  The GPU side
+(several contexts, the runtime pktio over ODP_AMD_GPUS, bench.py with two
+ranks) is tests/test_gpu_multi.py."""
 import os
 import socket
 
@@ -10,7 +14,7 @@ import numpy as np
 import torch.multiprocessing as mp
 
 from odp_amd import rules as R
-from odp_amd.shard import shard_bounds
+from odp_amd.shard import shard_bounds, shard_bounds_reference
 
 
 def _free_port():
@@ -73,6 +77,19 @@ def test_shard_bounds_balanced():
         w = np.minimum(lens, 128) + 22
         parts = [w[s:e].sum() for s, e in b]
         assert max(parts) - min(parts) <= 2 * 150   # each cut is within one packet
+
+
+def test_c_shard_matches_reference(built):
+    """mi_cls_shard (C, product) == the numpy restatement, including empty
+    batches, more shards than packets and uniform lengths."""
+    rng = np.random.default_rng(3)
+    for n in (0, 1, 2, 7, 64, 1000, 50_000):
+        for world in (1, 2, 3, 5, 8, 64):
+            for kind in ("imix", "60", "big"):
+                lens = (rng.choice([60, 566, 1514], n) if kind == "imix"
+                        else np.full(n, 60 if kind == "60" else 1514))
+                assert shard_bounds(lens, world) == shard_bounds_reference(lens, world), \
+                    (n, world, kind)
 
 
 def test_two_rank_shards_equal_single(built):
