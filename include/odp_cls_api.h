@@ -311,6 +311,12 @@ void odp_amd_cls_queue_stats_add(uint32_t cos_index, uint32_t slot, uint64_t pac
 /* cos->pool of a CoS index (pool switch of the receive path). */
 odp_pool_t odp_amd_cls_pool_of(uint32_t cos_index);
 
+/* Enqueue flavour of a CoS index (cos->vector): returns use_std_enq (1 plain
+ * enqueue, 0 packet vectors from *vec_pool of up to *vec_max packets), and
+ * *use_aggr (hash-queue runs go to odp_queue_aggr(dst, 0)); -1 if invalid. */
+int odp_amd_cls_cos_enq_mode(uint32_t cos_index, odp_pool_t *vec_pool, uint32_t *vec_max,
+			     int *use_aggr);
+
 /* packet_rss_hash (odp_classification.c:1773-1839) on a parsed frame;
  * hp = bit0 ipv4, bit1 ipv6, bit2 udp, bit3 tcp. */
 uint32_t odp_amd_cls_rss_hash(const uint8_t *base, uint64_t in_flags, uint32_t l3, uint32_t l4,

@@ -54,6 +54,7 @@ typedef struct _odp_abi_pktio_t  *odp_pktio_t;
 typedef struct _odp_abi_packet_t *odp_packet_t;
 typedef struct _odp_abi_event_t  *odp_event_t;
 typedef struct _odp_abi_evv_t    *odp_event_vector_t;
+typedef struct _odp_abi_pktv_t   *odp_packet_vector_t;
 typedef struct _odp_abi_shm_t    *odp_shm_t;
 typedef struct _odp_abi_pktin_t  *_odp_pktin_hdl_t;
 typedef uint64_t odp_instance_t;
@@ -66,6 +67,7 @@ typedef uint64_t odp_instance_t;
 #define ODP_PACKET_INVALID ((odp_packet_t)0)
 #define ODP_EVENT_INVALID  ((odp_event_t)0)
 #define ODP_EVENT_VECTOR_INVALID ((odp_event_vector_t)0)
+#define ODP_PACKET_VECTOR_INVALID ((odp_packet_vector_t)0)
 #define ODP_SHM_INVALID    ((odp_shm_t)0)
 
 #define ODP_COS_NAME_LEN    32
@@ -309,6 +311,18 @@ void odp_event_vector_size_set(odp_event_vector_t evv, uint32_t size);
 odp_event_type_t odp_event_vector_type(odp_event_vector_t evv);
 odp_pool_t odp_event_vector_pool(odp_event_vector_t evv);
 
+/* packet.h: packet vectors (ODP_POOL_VECTOR pools, ODP_EVENT_PACKET_VECTOR
+ * events); freeing a vector does not free its packets */
+odp_packet_vector_t odp_packet_vector_from_event(odp_event_t ev);
+odp_event_t odp_packet_vector_to_event(odp_packet_vector_t pktv);
+odp_packet_vector_t odp_packet_vector_alloc(odp_pool_t pool);
+void odp_packet_vector_free(odp_packet_vector_t pktv);
+uint32_t odp_packet_vector_tbl(odp_packet_vector_t pktv, odp_packet_t **pkt_tbl);
+uint32_t odp_packet_vector_size(odp_packet_vector_t pktv);
+void odp_packet_vector_size_set(odp_packet_vector_t pktv, uint32_t size);
+odp_pool_t odp_packet_vector_pool(odp_packet_vector_t pktv);
+int odp_packet_vector_valid(odp_packet_vector_t pktv);
+
 /* ------------------------------------------------------------ pools */
 typedef enum odp_pool_type_t {
 	ODP_POOL_BUFFER  = ODP_EVENT_BUFFER,
@@ -505,7 +519,8 @@ int odp_packet_has_ts(odp_packet_t pkt);
 /* ------------------------------------------------------------ queues */
 typedef enum odp_queue_type_t {
 	ODP_QUEUE_TYPE_PLAIN = 0,
-	ODP_QUEUE_TYPE_SCHED
+	ODP_QUEUE_TYPE_SCHED,
+	ODP_QUEUE_TYPE_AGGR     /* event aggregator of a queue (odp_queue_aggr) */
 } odp_queue_type_t;
 
 typedef enum odp_queue_op_mode_t {

@@ -28,6 +28,9 @@
 #include "odp_cls_api.h"
 #include "mi_cls.h"
 
+/* runtime (odp_rt.c): a handle of a queue the runtime created */
+int rt_queue_is_valid(odp_queue_t h);
+
 #define COS_QUEUE_MAX 32
 #define PMR_TERM_MAX 8
 #define MAX_MARK 0xFFFFu
@@ -70,6 +73,12 @@ typedef struct {
 	 * enqueue stage of the receive path */
 	uint64_t q_packets[COS_QUEUE_MAX];
 	uint64_t q_discards[COS_QUEUE_MAX];
+	/* cos->vector (odp_classification_datamodel.h:145-151): packet vector
+	 * delivery, or event-aggregator enqueue of hash-queue runs */
+	odp_pool_t vec_pool;
+	uint32_t vec_max;
+	int use_std_enq;
+	int use_aggr;
 } cos_t;
 
 typedef struct {
@@ -313,10 +322,38 @@ odp_cos_t odp_cls_cos_create(const char *name, const odp_cls_cos_param_t *param_
 	}
 	if (param.num_queue > COS_QUEUE_MAX || param.num_queue < 1)
 		return ODP_COS_INVALID;
+	/* event aggregation: the CoS queue is an aggregator, or its hash queues
+	 * get aggregators (:256-259) */
+	const int event_aggr_enabled =
+		(param.num_queue == 1 && param.queue != ODP_QUEUE_INVALID &&
+		 rt_queue_is_valid(param.queue) && odp_queue_type(param.queue) == ODP_QUEUE_TYPE_AGGR) ||
+		(param.num_queue > 1 && param.queue_param.num_aggr);
+
+	/* packet vector parameters (:261-288) */
 	if (param.vector.enable) {
-		/* packet vectors need the pool subsystem; not supported here */
-		ERR("packet vector delivery is not supported by this build\n");
-		return ODP_COS_INVALID;
+		odp_pool_info_t pool_info;
+
+		if (event_aggr_enabled) {
+			ERR("Packet and event vectoring enabled simultaneously\n");
+			return ODP_COS_INVALID;
+		}
+		if (param.vector.pool == ODP_POOL_INVALID ||
+		    odp_pool_info(param.vector.pool, &pool_info)) {
+			ERR("invalid packet vector pool\n");
+			return ODP_COS_INVALID;
+		}
+		if (pool_info.params.type != ODP_POOL_VECTOR) {
+			ERR("wrong pool type\n");
+			return ODP_COS_INVALID;
+		}
+		if (param.vector.max_size == 0) {
+			ERR("vector.max_size is zero\n");
+			return ODP_COS_INVALID;
+		}
+		if (param.vector.max_size > pool_info.params.vector.max_size) {
+			ERR("vector.max_size larger than pool max vector size\n");
+			return ODP_COS_INVALID;
+		}
 	}
 	if (param.aggr_enq_profile.type != ODP_AEP_TYPE_NONE)
 		return ODP_COS_INVALID;
@@ -369,6 +406,10 @@ odp_cos_t odp_cls_cos_create(const char *name, const odp_cls_cos_param_t *param_
 		c->valid = 1;
 		c->num_rule = 0;
 		c->index = (uint8_t)i;
+		c->vec_pool = param.vector.enable ? param.vector.pool : ODP_POOL_INVALID;
+		c->vec_max = param.vector.enable ? param.vector.max_size : 0;
+		c->use_std_enq = !param.vector.enable;
+		c->use_aggr = event_aggr_enabled && param.num_queue > 1;
 		c->stats_enable = param.stats_enable;
 		G.gen++;
 		ret = cos_hdl(i);
@@ -1194,6 +1235,23 @@ void odp_amd_cls_queue_stats_add(uint32_t cos_index, uint32_t slot, uint64_t pac
 		__atomic_fetch_add(&c->q_packets[slot], packets, __ATOMIC_RELAXED);
 	if (discards)
 		__atomic_fetch_add(&c->q_discards[slot], discards, __ATOMIC_RELAXED);
+}
+
+/* The enqueue flavour of a CoS (cos->vector, odp_classification.c:362-365):
+ * *vec_pool / *vec_max for packet vector delivery (use_std_enq == 0),
+ * *use_aggr for hash-queue runs redirected to odp_queue_aggr(dst, 0).
+ * Returns use_std_enq, or -1 for an invalid index. */
+int odp_amd_cls_cos_enq_mode(uint32_t cos_index, odp_pool_t *vec_pool, uint32_t *vec_max,
+			     int *use_aggr)
+{
+	if (!G.init || cos_index >= G.max_cos)
+		return -1;
+	const cos_t *c = &G.cos[cos_index];
+
+	*vec_pool = c->vec_pool;
+	*vec_max = c->vec_max;
+	*use_aggr = c->use_aggr;
+	return c->use_std_enq;
 }
 
 /* cos->pool of the final CoS (_odp_cls_classify_packet, :1760-1764) */

@@ -844,29 +844,113 @@ static void apply_layer(mi_cls_result_t *r, odp_proto_layer_t layer)
 
 /* Enqueue a run of classified packets (_odp_cos_enq,
  * odp_classification_internal.h:171-201) */
-static void cos_enq_run(odp_packet_t pk[], int num)
+/* Queue slot of dst inside the CoS (_odp_cos_queue_idx,
+ * odp_classification_internal.h:49-65): 0 for a single-queue CoS. */
+static uint32_t cos_slot_of(uint32_t cos_index, odp_queue_t dst)
 {
-	pkt_hdr_t *h = rt_pkt_hdr(pk[0]);
-	int r = odp_queue_enq_multi(h->dst_queue, (const odp_event_t *)(void *)pk, num);
-
-	if (r < 0)
-		r = 0;
-	if (r != num)
-		odp_packet_free_multi(&pk[r], num - r);
-	/* the queue slot is recovered from the CoS's queue table */
-	uint32_t slot = 0;
-	odp_cos_t cos = (odp_cos_t)(uintptr_t)(h->cos + 1u);
-	uint32_t nq = odp_cls_cos_num_queue(cos);
+	odp_cos_t cos = (odp_cos_t)(uintptr_t)(cos_index + 1u);
+	uint32_t nq = odp_cls_cos_num_queue(cos), slot = 0;
 
 	if (nq > 1) {
 		odp_queue_t qs[32];
 
 		odp_cls_cos_queues(cos, qs, 32);
 		for (uint32_t i = 0; i < nq; i++)
-			if (qs[i] == h->dst_queue)
+			if (qs[i] == dst)
 				slot = i;
 	}
-	odp_amd_cls_queue_stats_add(h->cos, slot, (uint64_t)r, (uint64_t)(num - r));
+	return slot;
+}
+
+/* _odp_cos_vector_enq (odp_classification_internal.h:83-137): the run goes
+ * into ceil(num / max_size) packet vectors, all full but the last; what the
+ * vector pool cannot hold is counted as discards.  (The reference leaves the
+ * packets it could not place unreferenced; here they are freed.) */
+static void cos_vector_enq(odp_queue_t queue, odp_packet_t pk[], int num, uint32_t cos,
+			   odp_pool_t vpool, uint32_t max_size)
+{
+	const uint32_t slot = cos_slot_of(cos, queue);
+	int num_pktv = (int)(((uint32_t)num + max_size - 1) / max_size);
+	odp_event_t ev[num_pktv];
+	odp_packet_vector_t pv[num_pktv];
+	int i;
+
+	for (i = 0; i < num_pktv; i++) {
+		pv[i] = odp_packet_vector_alloc(vpool);
+		if (pv[i] == ODP_PACKET_VECTOR_INVALID)
+			break;
+		ev[i] = odp_packet_vector_to_event(pv[i]);
+	}
+	if (i == 0) {
+		odp_packet_free_multi(pk, num);
+		odp_amd_cls_queue_stats_add(cos, slot, 0, (uint64_t)num);
+		return;
+	}
+	num_pktv = i;
+	uint32_t num_enq = 0;
+
+	for (i = 0; i < num_pktv; i++) {
+		odp_packet_t *tbl;
+		uint32_t sz = max_size;
+
+		if (num_enq + max_size > (uint32_t)num)
+			sz = (uint32_t)num - num_enq;
+		odp_packet_vector_tbl(pv[i], &tbl);
+		memcpy(tbl, &pk[num_enq], sz * sizeof(odp_packet_t));
+		odp_packet_vector_size_set(pv[i], sz);
+		num_enq += sz;
+	}
+	if (num_enq < (uint32_t)num)
+		odp_packet_free_multi(&pk[num_enq], num - (int)num_enq);
+	int ret = odp_queue_enq_multi(queue, ev, num_pktv);
+
+	if (ret == num_pktv) {
+		odp_amd_cls_queue_stats_add(cos, slot, num_enq, (uint64_t)num - num_enq);
+		return;
+	}
+	if (ret < 0)
+		ret = 0;
+	uint32_t enqueued = max_size * (uint32_t)ret;
+
+	odp_amd_cls_queue_stats_add(cos, slot, enqueued, (uint64_t)num - enqueued);
+	for (i = ret; i < num_pktv; i++) {
+		odp_packet_t *tbl;
+		uint32_t sz = odp_packet_vector_tbl(pv[i], &tbl);
+
+		odp_packet_free_multi(tbl, (int)sz);
+		odp_packet_vector_free(pv[i]);
+	}
+}
+
+/* One enqueue run (equal dst_queue and cos): _odp_cos_enq
+ * (odp_classification_internal.h:142-167).  Single packets and CoS without
+ * packet vectors take the plain enqueue -- to odp_queue_aggr(dst, 0) for a
+ * hash-queue CoS with event aggregators -- others go into packet vectors;
+ * queue stats are kept on the CoS queue (dst). */
+static void cos_enq_run(odp_packet_t pk[], int num)
+{
+	pkt_hdr_t *h = rt_pkt_hdr(pk[0]);
+	const uint32_t cos = h->cos;
+	odp_queue_t dst = h->dst_queue;
+	odp_pool_t vpool;
+	uint32_t vmax;
+	int use_aggr;
+	const int std = odp_amd_cls_cos_enq_mode(cos, &vpool, &vmax, &use_aggr);
+
+	if (num < 2 || std != 0) {
+		odp_queue_t q = use_aggr ? odp_queue_aggr(dst, 0) : dst;
+		int r = q == ODP_QUEUE_INVALID ? -1
+			: odp_queue_enq_multi(q, (const odp_event_t *)(void *)pk, num);
+
+		if (r < 0)
+			r = 0;
+		if (r != num)
+			odp_packet_free_multi(&pk[r], num - r);
+		odp_amd_cls_queue_stats_add(cos, cos_slot_of(cos, dst), (uint64_t)r,
+					    (uint64_t)(num - r));
+		return;
+	}
+	cos_vector_enq(dst, pk, num, cos, vpool, vmax);
 }
 
 /* Pull up to `max` frames from the driver into the staging buffer (64 B

@@ -1149,10 +1149,71 @@ odp_event_type_t odp_event_vector_type(odp_event_vector_t v)
 	return t;
 }
 
+/* packet vectors (packet.h): event vectors of packets drawn from
+ * ODP_POOL_VECTOR pools; odp_packet_t and odp_event_t share their handles, so
+ * the vector's table serves both */
+odp_packet_vector_t odp_packet_vector_from_event(odp_event_t ev) { return (odp_packet_vector_t)(void *)ev; }
+odp_event_t odp_packet_vector_to_event(odp_packet_vector_t v) { return (odp_event_t)(void *)v; }
+
+odp_packet_vector_t odp_packet_vector_alloc(odp_pool_t pool)
+{
+	rt_pool_t *p = rt_pool(pool);
+
+	if (!p || p->param.type != ODP_POOL_VECTOR)
+		return ODP_PACKET_VECTOR_INVALID;
+	return (odp_packet_vector_t)(void *)odp_event_vector_alloc(pool);
+}
+
+void odp_packet_vector_free(odp_packet_vector_t v)
+{
+	odp_event_vector_free((odp_event_vector_t)(void *)v);
+}
+
+uint32_t odp_packet_vector_tbl(odp_packet_vector_t v, odp_packet_t **tbl)
+{
+	*tbl = (odp_packet_t *)(void *)evv((odp_event_vector_t)(void *)v)->tbl;
+	return evv((odp_event_vector_t)(void *)v)->size;
+}
+
+uint32_t odp_packet_vector_size(odp_packet_vector_t v)
+{
+	return evv((odp_event_vector_t)(void *)v)->size;
+}
+
+void odp_packet_vector_size_set(odp_packet_vector_t v, uint32_t size)
+{
+	evv((odp_event_vector_t)(void *)v)->size = size;
+}
+
+odp_pool_t odp_packet_vector_pool(odp_packet_vector_t v)
+{
+	return odp_event_vector_pool((odp_event_vector_t)(void *)v);
+}
+
+int odp_packet_vector_valid(odp_packet_vector_t v)
+{
+	if (v == ODP_PACKET_VECTOR_INVALID)
+		return 0;
+	const ev_hdr_t *h = &evv((odp_event_vector_t)(void *)v)->ev;
+
+	return h->type == ODP_EVENT_PACKET_VECTOR &&
+	       evv((odp_event_vector_t)(void *)v)->size <= evv((odp_event_vector_t)(void *)v)->max_size;
+}
+
 /* ================================================================ queues */
 static rt_queue_t *rtq(odp_queue_t h)
 {
 	return (rt_queue_t *)(void *)h;
+}
+
+/* a handle of a queue this runtime created (the classifier is also driven
+ * with foreign queue handles by tests and applications of its C ABI) */
+int rt_queue_is_valid(odp_queue_t h)
+{
+	const rt_queue_t *q = rtq(h);
+
+	return q >= &RT.queue[0] && q < &RT.queue[RT_MAX_QUEUES] &&
+	       ((uintptr_t)q - (uintptr_t)&RT.queue[0]) % sizeof(rt_queue_t) == 0 && q->used;
 }
 
 void odp_queue_param_init(odp_queue_param_t *p)
@@ -1473,7 +1534,10 @@ odp_event_t odp_queue_deq(odp_queue_t h)
 	return odp_queue_deq_multi(h, &e, 1) == 1 ? e : ODP_EVENT_INVALID;
 }
 
-odp_queue_type_t odp_queue_type(odp_queue_t h) { return rtq(h)->param.type; }
+odp_queue_type_t odp_queue_type(odp_queue_t h)
+{
+	return rtq(h)->is_aggr ? ODP_QUEUE_TYPE_AGGR : rtq(h)->param.type;
+}
 odp_schedule_sync_t odp_queue_sched_type(odp_queue_t h) { return rtq(h)->param.sched.sync; }
 odp_schedule_prio_t odp_queue_sched_prio(odp_queue_t h) { return rtq(h)->param.sched.prio; }
 void *odp_queue_context(odp_queue_t h) { return rtq(h)->context; }

@@ -105,5 +105,6 @@ int rt_thread_id(void);
 int rt_pktio_sched_poll(void);
 int rt_pktio_poll_index(int idx);
 uint32_t rt_gpu_index(void);
+int rt_queue_is_valid(odp_queue_t h);
 
 #endif /* ODP_AMD_RT_INTERNAL_H_ */

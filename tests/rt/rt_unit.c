@@ -302,6 +302,95 @@ static void t_misc(void)
 	      odp_be_to_cpu_32(0x11223344) == 0x44332211u);
 }
 
+/* packet vectors (packet.h) and CoS vector parameter validation
+ * (odp_cls_cos_create, odp_classification.c:256-288) */
+static void t_vectors(odp_pool_t pool)
+{
+	odp_pool_param_t vp;
+
+	odp_pool_param_init(&vp);
+	vp.type = ODP_POOL_VECTOR;
+	vp.vector.num = 2;
+	vp.vector.max_size = 8;
+	odp_pool_t vpool = odp_pool_create("pktv", &vp);
+	odp_packet_vector_t v1 = odp_packet_vector_alloc(vpool), v2 = odp_packet_vector_alloc(vpool);
+
+	CHECK("pktv.alloc", v1 != ODP_PACKET_VECTOR_INVALID && v2 != ODP_PACKET_VECTOR_INVALID);
+	CHECK("pktv.exhausted", odp_packet_vector_alloc(vpool) == ODP_PACKET_VECTOR_INVALID);
+	CHECK("pktv.event_type",
+	      odp_event_type(odp_packet_vector_to_event(v1)) == ODP_EVENT_PACKET_VECTOR);
+	CHECK("pktv.from_event",
+	      odp_packet_vector_from_event(odp_packet_vector_to_event(v1)) == v1);
+	odp_packet_t *tbl;
+
+	CHECK("pktv.empty", odp_packet_vector_tbl(v1, &tbl) == 0 && odp_packet_vector_valid(v1));
+	tbl[0] = odp_packet_alloc(pool, 60);
+	tbl[1] = odp_packet_alloc(pool, 60);
+	odp_packet_vector_size_set(v1, 2);
+	CHECK("pktv.size", odp_packet_vector_size(v1) == 2 && odp_packet_vector_pool(v1) == vpool);
+	odp_packet_free_multi(tbl, 2);
+	odp_packet_vector_free(v1);
+	odp_packet_vector_free(v2);
+	/* a packet pool is no vector pool */
+	CHECK("pktv.wrong_pool", odp_packet_vector_alloc(pool) == ODP_PACKET_VECTOR_INVALID);
+
+	/* CoS vector parameters */
+	odp_queue_param_t qp;
+	odp_cls_cos_param_t cp;
+
+	odp_queue_param_init(&qp);
+	qp.type = ODP_QUEUE_TYPE_SCHED;
+	odp_queue_t q = odp_queue_create("vq", &qp);
+
+	odp_cls_cos_param_init(&cp);
+	cp.queue = q;
+	cp.vector.enable = true;
+	cp.vector.pool = ODP_POOL_INVALID;
+	cp.vector.max_size = 4;
+	CHECK("cosv.no_pool", odp_cls_cos_create("v0", &cp) == ODP_COS_INVALID);
+	cp.vector.pool = pool;
+	CHECK("cosv.wrong_pool_type", odp_cls_cos_create("v1", &cp) == ODP_COS_INVALID);
+	cp.vector.pool = vpool;
+	cp.vector.max_size = 0;
+	CHECK("cosv.max_size_zero", odp_cls_cos_create("v2", &cp) == ODP_COS_INVALID);
+	cp.vector.max_size = 9;
+	CHECK("cosv.max_size_above_pool", odp_cls_cos_create("v3", &cp) == ODP_COS_INVALID);
+	cp.vector.max_size = 8;
+	odp_cos_t ok = odp_cls_cos_create("v4", &cp);
+
+	CHECK("cosv.ok", ok != ODP_COS_INVALID);
+	odp_cos_destroy(ok);
+	/* packet vectors together with event aggregation (hash queues with
+	 * aggregators) */
+	odp_pool_param_t ep;
+	odp_event_aggr_config_t ac;
+
+	odp_pool_param_init(&ep);
+	ep.type = ODP_POOL_EVENT_VECTOR;
+	ep.event_vector.num = 4;
+	ep.event_vector.max_size = 4;
+	memset(&ac, 0, sizeof(ac));
+	ac.pool = odp_pool_create("evq", &ep);
+	ac.max_size = 4;
+	ac.event_type = ODP_EVENT_PACKET;
+	odp_cls_cos_param_init(&cp);
+	cp.num_queue = 4;
+	cp.queue_param = qp;
+	cp.queue_param.num_aggr = 1;
+	cp.queue_param.aggr = &ac;
+	cp.vector.enable = true;
+	cp.vector.pool = vpool;
+	cp.vector.max_size = 4;
+	CHECK("cosv.pktv_and_aggr", odp_cls_cos_create("v5", &cp) == ODP_COS_INVALID);
+	cp.vector.enable = false;
+	ok = odp_cls_cos_create("v6", &cp);
+	CHECK("cosv.aggr_hash_queues", ok != ODP_COS_INVALID);
+	odp_cos_destroy(ok);
+	odp_queue_destroy(q);
+	odp_pool_destroy(vpool);
+	odp_pool_destroy(ac.pool);
+}
+
 int main(int argc, char *argv[])
 {
 	odp_instance_t inst;
@@ -321,6 +410,7 @@ int main(int argc, char *argv[])
 	t_sched(pool);
 	t_atomic(inst, pool);
 	t_aggr(pool);
+	t_vectors(pool);
 	t_misc();
 	odp_pool_destroy(pool);
 	odp_term_local();

@@ -12,7 +12,13 @@
  *   <pktio> = "pcap:in=FILE..." or "loop" (then the frames of the source
  *   pcap are read through a second, parse-less pcap pktio and sent into the
  *   loop interface).
+ * environment: RX_PKTV=<max_size>,<vectors>  every enqueue CoS delivers packet
+ *   vectors (cls_cos_param.vector) from a vector pool of that size;
+ *   RX_AGGR=<max_size>  hash-queue CoS get one event aggregator per queue
+ *   (queue_param.num_aggr), so their runs go to odp_queue_aggr(q, 0).
  * output lines:
+ *   V <queue> <size> / E <queue> <size>   a packet / event vector; its
+ *                                         packets follow as P lines
  *   P <queue> <pool> <in_flags> <err> <l3> <l4> <cos> <mark> <hex frame>
  *   S <in_packets> <in_errors> <in_discards> <in_octets>
  *   Q <cos> <slot> <packets> <discards>     (odp_cls_queue_stats)
@@ -22,6 +28,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include "odp_api.h"
 
@@ -35,6 +42,9 @@ static char cos_name[MAX_COS][ODP_COS_NAME_LEN];
 static int ncos;
 static odp_pmr_t pmr_h[MAX_PMR];
 static int npmr;
+static odp_pool_t pktv_pool = ODP_POOL_INVALID, evv_pool = ODP_POOL_INVALID;
+static uint32_t pktv_max, aggr_max;
+static odp_event_aggr_config_t aggr_cfg;
 
 static int hexval(char c)
 {
@@ -93,7 +103,16 @@ static int replay(FILE *f, odp_pktio_t pktio, int cos_pools)
 			cp.num_queue = (uint32_t)nq;
 			snprintf(cos_name[ncos], ODP_COS_NAME_LEN, "%s", name);
 			if (!action) {
+				if (pktv_pool != ODP_POOL_INVALID) {
+					cp.vector.enable = true;
+					cp.vector.pool = pktv_pool;
+					cp.vector.max_size = pktv_max;
+				}
 				if (nq > 1) {
+					if (evv_pool != ODP_POOL_INVALID) {
+						qp.num_aggr = 1;
+						qp.aggr = &aggr_cfg;
+					}
 					cp.queue_param = qp;
 					cp.hash_proto.all_bits = hp;
 				} else {
@@ -164,6 +183,41 @@ static const char *poolname(odp_pool_t p)
 	return odp_pool_info(p, &info) == 0 ? info.name : "?";
 }
 
+static void print_pkt(const char *q, odp_packet_t pkt);
+
+/* one received event: a packet, or a packet / event vector of packets */
+static void print_ev(const char *q, odp_event_t ev)
+{
+	if (odp_event_type(ev) == ODP_EVENT_PACKET_VECTOR) {
+		odp_packet_vector_t v = odp_packet_vector_from_event(ev);
+		odp_packet_t *tbl;
+		uint32_t n = odp_packet_vector_tbl(v, &tbl);
+
+		printf("V %s %u\n", q, n);
+		for (uint32_t i = 0; i < n; i++) {
+			print_pkt(q, tbl[i]);
+			odp_packet_free(tbl[i]);
+		}
+		odp_packet_vector_free(v);
+		return;
+	}
+	if (odp_event_type(ev) == ODP_EVENT_VECTOR) {
+		odp_event_vector_t v = odp_event_vector_from_event(ev);
+		odp_event_t *tbl;
+		uint32_t n = odp_event_vector_tbl(v, &tbl);
+
+		printf("E %s %u\n", q, n);
+		for (uint32_t i = 0; i < n; i++) {
+			print_pkt(q, odp_packet_from_event(tbl[i]));
+			odp_event_free(tbl[i]);
+		}
+		odp_event_vector_free(v);
+		return;
+	}
+	print_pkt(q, odp_packet_from_event(ev));
+	odp_event_free(ev);
+}
+
 static void print_pkt(const char *q, odp_packet_t pkt)
 {
 	uint32_t len = odp_packet_len(pkt);
@@ -216,6 +270,38 @@ int main(int argc, char *argv[])
 		return 3;
 	odp_schedule_config(NULL);
 	odp_pool_t pool = mkpool("pktio_pool");
+
+	if (getenv("RX_PKTV")) {
+		odp_pool_param_t vp;
+		unsigned mx = 0, num = 0;
+
+		sscanf(getenv("RX_PKTV"), "%u,%u", &mx, &num);
+		odp_pool_param_init(&vp);
+		vp.type = ODP_POOL_VECTOR;
+		vp.vector.num = num;
+		vp.vector.max_size = mx;
+		pktv_pool = odp_pool_create("pktv_pool", &vp);
+		pktv_max = mx;
+		if (pktv_pool == ODP_POOL_INVALID)
+			return 12;
+	}
+	if (getenv("RX_AGGR")) {
+		odp_pool_param_t vp;
+
+		aggr_max = (uint32_t)atoi(getenv("RX_AGGR"));
+		odp_pool_param_init(&vp);
+		vp.type = ODP_POOL_EVENT_VECTOR;
+		vp.event_vector.num = 20000;
+		vp.event_vector.max_size = aggr_max;
+		evv_pool = odp_pool_create("evv_pool", &vp);
+		if (evv_pool == ODP_POOL_INVALID)
+			return 13;
+		memset(&aggr_cfg, 0, sizeof(aggr_cfg));
+		aggr_cfg.pool = evv_pool;
+		aggr_cfg.max_size = aggr_max;
+		aggr_cfg.max_tmo_ns = 1000;
+		aggr_cfg.event_type = ODP_EVENT_PACKET;
+	}
 
 	odp_pktio_param_init(&pp);
 	pp.in_mode = strcmp(mode, "sched") == 0 ? ODP_PKTIN_MODE_SCHED :
@@ -304,10 +390,8 @@ int main(int argc, char *argv[])
 			n = odp_schedule_multi(&from, ODP_SCHED_NO_WAIT, ev, 64);
 			if (n <= 0)
 				break;
-			for (int i = 0; i < n; i++) {
-				print_pkt(qname(from), odp_packet_from_event(ev[i]));
-				odp_event_free(ev[i]);
-			}
+			for (int i = 0; i < n; i++)
+				print_ev(qname(from), ev[i]);
 		}
 	} else {
 		int idle = 0;
@@ -327,11 +411,11 @@ int main(int argc, char *argv[])
 			} else {
 				n = odp_schedule_multi(&from, ODP_SCHED_NO_WAIT, ev, 64);
 			}
-			for (int i = 0; i < n; i++) {
-				print_pkt(qname(from), odp_packet_from_event(ev[i]));
-				odp_event_free(ev[i]);
-			}
+			for (int i = 0; i < n; i++)
+				print_ev(qname(from), ev[i]);
 			idle = (n <= 0 && odp_amd_pktio_rx_idle(pktio) == 1) ? idle + 1 : 0;
+			if (n <= 0 && evv_pool != ODP_POOL_INVALID)
+				usleep(2000);   /* let the aggregators' max_tmo_ns pass */
 		}
 	}
 	odp_pktio_stats_t st;

@@ -75,7 +75,10 @@ def write_rules(path, prog):
 
 # ------------------------------------------------------------------ driver
 def run_driver(pktio, rules_path, mode="sched", layer=4, cos_pools=1, cls=1, src=None,
-               env=None, timeout=120):
+               env=None, timeout=120, events=None):
+    """events: a dict that receives, per queue, the delivery structure in
+    order -- ("P",) a plain packet, ("V", n) / ("E", n) a packet / event
+    vector of n packets (its packets are in the queue's packet list)."""
     args = [DRIVER, pktio, rules_path or "-", mode, str(layer), str(cos_pools), str(cls)]
     if src:
         args.append(src)
@@ -87,11 +90,21 @@ def run_driver(pktio, rules_path, mode="sched", layer=4, cos_pools=1, cls=1, src
     queues = defaultdict(list)
     stats = None
     qstats = {}
+    inside = defaultdict(int)   # packets still expected inside the last vector
     for line in r.stdout.splitlines():
         p = line.split()
         if not p:
             continue
+        if p[0] in ("V", "E"):
+            if events is not None:
+                events.setdefault(p[1], []).append((p[0], int(p[2])))
+            inside[p[1]] = int(p[2])
+            continue
         if p[0] == "P":
+            if inside[p[1]]:
+                inside[p[1]] -= 1
+            elif events is not None:
+                events.setdefault(p[1], []).append(("P",))
             q, pool, fl, err, l3, l4, mark, ln, data = p[1:10]
             queues[q].append((pool, int(fl, 16), int(err), int(l3), int(l4), int(mark),
                               int(ln), data))
@@ -180,6 +193,50 @@ def expected(prog, frames, cos_pools=1, cls=1, layer=4, pktin_queue="odp-pktin-0
         fl_rep = (fl & FLAG_MASK) | (l3st << 40) | (l4st << 42)
         queues[q].append((pool, fl_rep, int(err != 0), l3, l4, mark, len(fr), fr.hex()))
     return dict(queues), (in_pk, in_err, in_disc, octets), dict(qstats)
+
+
+def expected_vectors(prog, frames, burst, max_size):
+    """Per queue, the packet-vector delivery the receive path makes with
+    packet vectors on every enqueue CoS (_odp_cos_enq / _odp_cos_vector_enq,
+    odp_classification_internal.h:83-167): frames arrive in bursts of `burst`;
+    inside a burst, consecutive enqueued packets with the same queue and CoS
+    form a run (dropped packets do not end one; a burst's end does); a run of
+    one is a plain packet, a longer run ceil(L / max_size) vectors, all full
+    but the last."""
+    from oracle.oracle import Oracle
+    o = Oracle()
+    o.apply(prog)
+    recs = o.classify(pg.batch_from_frames(frames))
+    slots = cos_names(prog)
+    ev = defaultdict(list)
+
+    def flush(key, n):
+        if not n:
+            return
+        q = key[0]
+        if n == 1:
+            ev[q].append(("P",))
+            return
+        while n:
+            k = min(n, max_size)
+            ev[q].append(("V", k))
+            n -= k
+
+    for b0 in range(0, len(frames), burst):
+        key, n = None, 0
+        for r in recs[b0: b0 + burst]:
+            if int(r["outcome"]) != R.OUT_ENQ:
+                continue
+            name, attrs = slots[int(r["cos"])]
+            q = name if attrs["num_queue"] == 1 else f"_odp_cos_hq_{int(r['cos'])}_{int(r['queue'])}"
+            k = (q, int(r["cos"]))
+            if k != key:
+                flush(key, n) if key else None
+                key, n = k, 0
+            n += 1
+        if key:
+            flush(key, n)
+    return dict(ev)
 
 
 def compare(got, exp):

@@ -138,3 +138,69 @@ def test_rx_config2_traffic(built, gpu, tmp_path):
     frames = [b.frame(i) for i in range(b.n)]
     got = _run_case(tmp_path, prog, frames)
     assert sum(len(v) for v in got[0].values()) == 20000
+
+
+@pytest.mark.parametrize("max_size,burst", [(4, 37), (1, 64), (64, 4096), (7, 1)])
+def test_rx_packet_vector_cos(built, gpu, tmp_path, max_size, burst):
+    """CoS packet-vector delivery (odp_cls_cos_param_t.vector): the same
+    packets, order, metadata and counters as plain delivery, grouped into
+    vectors exactly as _odp_cos_vector_enq groups each enqueue run
+    (odp_classification_internal.h:83-137)."""
+    frames = H.pcap_frames([f for _, f in zoo.all_frames()] * 3)
+    prog = zoo.prog_everything()
+    pc = str(tmp_path / "in.pcap")
+    H.write_pcap(pc, frames)
+    rules = str(tmp_path / "rules.txt")
+    H.write_rules(rules, prog)
+    ev = {}
+    got = H.run_driver(f"pcap:in={pc}", rules, "sched", 4, 1, 1, events=ev,
+                       env={"RX_PKTV": f"{max_size},100000", "ODP_AMD_RX_BURST": str(burst)})
+    H.compare(got, H.expected(prog, frames, 1, 1, 4))
+    exp = H.expected_vectors(prog, frames, burst, max_size)
+    assert ev == exp
+
+
+def test_rx_packet_vector_pool_exhausted(built, gpu, tmp_path):
+    """A vector pool too small for the traffic: runs that get no vector are
+    dropped and counted as queue discards (odp_classification_internal.h:
+    104-108); nothing is lost without a count."""
+    frames = H.pcap_frames([f for _, f in zoo.all_frames()] * 4)
+    prog = zoo.prog_everything()
+    pc = str(tmp_path / "in.pcap")
+    H.write_pcap(pc, frames)
+    rules = str(tmp_path / "rules.txt")
+    H.write_rules(rules, prog)
+    queues, stats, qstats = H.run_driver(f"pcap:in={pc}", rules, "sched", 4, 1, 1,
+                                         env={"RX_PKTV": "8,1", "ODP_AMD_RX_BURST": "4096"})
+    _, _, eqs = H.expected(prog, frames, 1, 1, 4)
+    delivered = sum(len(v) for v in queues.values())
+    discards = sum(d for _, d in qstats.values())
+    assert delivered + discards == sum(v[0] for v in eqs.values())
+    assert discards > 0
+
+
+def test_rx_hash_queue_event_aggregators(built, gpu, tmp_path):
+    """Hash-queue CoS whose queues have event aggregators
+    (queue_param.num_aggr): runs go to odp_queue_aggr(q, 0)
+    (odp_classification_internal.h:149-157), so every packet of those queues
+    arrives inside an event vector; order, metadata and queue stats as plain
+    delivery."""
+    frames = H.pcap_frames([f for _, f in zoo.all_frames()] * 3)
+    prog = zoo.prog_everything()
+    assert any(op[0] == "cos" and op[2]["num_queue"] > 1 for op in prog)
+    pc = str(tmp_path / "in.pcap")
+    H.write_pcap(pc, frames)
+    rules = str(tmp_path / "rules.txt")
+    H.write_rules(rules, prog)
+    ev = {}
+    got = H.run_driver(f"pcap:in={pc}", rules, "sched", 4, 1, 1, events=ev,
+                       env={"RX_AGGR": "8", "ODP_AMD_RX_BURST": "41"})
+    H.compare(got, H.expected(prog, frames, 1, 1, 4))
+    hq = [q for q in got[0] if q.startswith("_odp_cos_hq_")]
+    assert hq
+    for q in hq:
+        assert all(e[0] == "E" and 1 <= e[1] <= 8 for e in ev[q]), ev[q]
+        assert sum(e[1] for e in ev[q]) == len(got[0][q])
+    for q in got[0]:
+        if q not in hq:
+            assert all(e == ("P",) for e in ev[q])
