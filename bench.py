@@ -219,9 +219,84 @@ def time_e2e(c, batch, dev, steps=5):
     torch.cuda.synchronize(dev)
     dt = (time.perf_counter() - t0) / steps
     h2d = batch.buf.nbytes + 6 * batch.n
-    return {"mpkts_per_s": batch.n / dt / 1e6, "ms_per_step": dt * 1e3,
-            "h2d_bytes": int(h2d), "d2h_bytes": 16 * batch.n,
-            "note": "pinned H2D of the whole packed batch + descriptors, kernel, D2H results"}
+    out = {"copy": {"mpkts_per_s": round(batch.n / dt / 1e6, 2), "ms_per_step": round(dt * 1e3, 4),
+                    "h2d_bytes": int(h2d), "d2h_bytes": 16 * batch.n,
+                    "note": "pinned H2D of the whole packed batch + descriptors, kernel, "
+                            "D2H of the records"}}
+    # zero copy: the kernel reads the packets' header windows and the
+    # descriptors straight from page-locked host memory over PCIe and writes
+    # the records back the same way -- no staging copy, only the bytes the
+    # kernel reads cross the link
+    from odp_amd import cls
+    hb = cls.PinnedArray(batch.buf.nbytes + 64)
+    ho = cls.PinnedArray(4 * batch.n)
+    hl = cls.PinnedArray(2 * batch.n)
+    hr = cls.PinnedArray(16 * batch.n)
+    try:
+        hb.u8[: batch.buf.nbytes] = batch.buf
+        ho.view(np.uint32)[:] = batch.off
+        hl.view(np.uint16)[:] = batch.len
+
+        def zstep():
+            assert c.classify_device(hb.ptr, ho.ptr, hl.ptr, batch.n, hr.ptr, sp) == 0
+        zstep()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            zstep()
+        torch.cuda.synchronize(dev)
+        dz = (time.perf_counter() - t0) / steps
+        same = bool(np.array_equal(hr.view(np.uint8, 16 * batch.n),
+                                   h_out.numpy().view(np.uint8).reshape(-1)))
+        out["zero_copy"] = {"mpkts_per_s": round(batch.n / dz / 1e6, 2),
+                            "ms_per_step": round(dz * 1e3, 4),
+                            "link_bytes": int(batch.header_bytes()),
+                            "records_equal_copy_path": same,
+                            "note": "kernel reads header windows + descriptors from pinned host "
+                                    "memory and writes the records there (no staging copy)"}
+    finally:
+        for a in (hb, ho, hl, hr):
+            a.close()
+    return out
+
+
+def time_runtime(batch, prog, n_frames=200_000, loops=10):
+    """Packets / s through the ODP runtime's receive path on this batch's
+    traffic: a pcap pktio replaying n_frames frames `loops` times, GPU
+    classification per burst (odp_amd_cls_classify_host), CoS enqueue and
+    the application draining the queues -- through odp_pktin_recv (DIRECT)
+    and through the scheduler (SCHED).  tests/_bin/rx_driver in rate mode."""
+    import subprocess
+    import tempfile
+    from tests import rt_helpers as H
+    n = min(n_frames, batch.n)
+    frames = [batch.frame(i) for i in range(n)]
+    out = {}
+    with tempfile.TemporaryDirectory() as td:
+        pc = os.path.join(td, "in.pcap")
+        rules = os.path.join(td, "rules.txt")
+        H.write_pcap(pc, frames)
+        H.write_rules(rules, prog)
+        for mode in ("direct", "sched"):
+            env = dict(os.environ, RX_COUNT_ONLY="1")
+            r = subprocess.run([H.DRIVER, f"pcap:in={pc}:loops={loops}", rules, mode, "4", "0",
+                                "1"], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                               timeout=300, env=env)
+            line = [ln for ln in r.stdout.splitlines() if ln.startswith("R ")]
+            if r.returncode or not line:
+                out[mode] = {"error": (r.stderr or r.stdout)[-300:]}
+                continue
+            pk, ns = (int(x) for x in line[-1].split()[1:3])
+            out[mode] = {"mpkts_per_s": round(pk / ns * 1e3, 3), "packets_delivered": pk}
+            st = [ln for ln in r.stdout.splitlines() if ln.startswith("S ")]
+            if st:
+                v = [int(x) for x in st[-1].split()[1:5]]
+                out[mode].update(in_packets=v[0], in_errors=v[1], in_discards=v[2])
+    out["note"] = (f"ODP runtime receive path ({n} frames x {loops} loops of this workload's "
+                   f"traffic, pcap pktio, 4096-frame GPU bursts, CoS enqueue, one application "
+                   f"thread draining the queues): odp_pktin_recv (direct) and odp_schedule "
+                   f"(sched)")
+    return out
 
 
 def cpu_baseline(prog, batch, seconds):
@@ -425,6 +500,10 @@ def main():
                 line["e2e"] = time_e2e(c, batch, dev)
             except Exception as e:   # recorded, never fatal
                 line["e2e"] = {"error": str(e)}
+            try:
+                line["e2e"]["runtime"] = time_runtime(batch, prog)
+            except Exception as e:   # recorded, never fatal
+                line["e2e"]["runtime"] = {"error": str(e)}
             if not a.no_cpu:
                 line["cpu_baseline"] = cpu_baseline(prog, batch, a.cpu_seconds)
             if not a.no_extra:

@@ -133,6 +133,8 @@ def _load():
         "odp_amd_cls_pktio_create_multi": (vp, [C.POINTER(i32), i32]),
         "odp_amd_cls_classify_host": (i32, [vp, vp, C.c_size_t, vp, vp, u32, vp, i32]),
         "mi_cls_shard": (i32, [vp, u32, u32, vp]),
+        "mi_cls_host_alloc": (vp, [C.c_size_t]),
+        "mi_cls_host_free": (None, [vp]),
         "odp_amd_cls_pktio_destroy": (i32, [vp]),
         "odp_amd_cls_compile": (C.c_long, [vp, vp, C.c_size_t]),
         "odp_amd_cls_classify": (i32, [vp, vp, vp, vp, u32, vp, vp]),
@@ -166,6 +168,27 @@ def shard(lens: np.ndarray, nshards: int) -> np.ndarray:
     if rc:
         raise RuntimeError(f"mi_cls_shard: {rc}")
     return begin
+
+
+class PinnedArray:
+    """numpy view of page-locked host memory from mi_cls_host_alloc
+    (hipHostMalloc): the GPU reads and writes it in place (zero copy)."""
+
+    def __init__(self, nbytes: int):
+        self.ptr = lib().mi_cls_host_alloc(max(1, nbytes))
+        if not self.ptr:
+            raise MemoryError("mi_cls_host_alloc failed")
+        self.nbytes = nbytes
+        self.u8 = np.ctypeslib.as_array((C.c_uint8 * max(1, nbytes)).from_address(self.ptr))
+
+    def view(self, dtype, count=None):
+        a = self.u8.view(dtype)
+        return a if count is None else a[:count]
+
+    def close(self):
+        if self.ptr:
+            lib().mi_cls_host_free(self.ptr)
+            self.ptr = None
 
 
 def lib():

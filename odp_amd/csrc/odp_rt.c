@@ -1700,6 +1700,8 @@ static int sched_try(odp_queue_t *from, odp_event_t ev[], int num)
 	return 0;
 }
 
+static __thread uint64_t tls_last_poll;
+
 int odp_schedule_multi(odp_queue_t *from, uint64_t wait, odp_event_t ev[], int num)
 {
 	uint64_t t_end = 0;
@@ -1709,9 +1711,20 @@ int odp_schedule_multi(odp_queue_t *from, uint64_t wait, odp_event_t ev[], int n
 	if (num <= 0 || tls_paused)
 		return 0;
 	for (;;) {
-		/* packet input first: a GPU burst feeds the CoS queues */
-		rt_pktio_sched_poll();
+		/* Queued events first; packet input (a GPU burst of up to 4096 frames
+		 * into the CoS queues) when they are drained, or at least every
+		 * millisecond so a busy event loop does not starve packet input.
+		 * Polling on every call would pile bursts up faster than the
+		 * application consumes them and run the pools dry. */
+		uint64_t t0 = now_ns();
+
 		got = sched_try(from, ev, num);
+		if (got <= 0 || t0 - tls_last_poll > 1000000) {
+			tls_last_poll = t0;
+			rt_pktio_sched_poll();
+			if (got <= 0)
+				got = sched_try(from, ev, num);
+		}
 		if (got > 0)
 			return got;
 		if (wait == ODP_SCHED_NO_WAIT)

@@ -22,6 +22,8 @@
  *   P <queue> <pool> <in_flags> <err> <l3> <l4> <cos> <mark> <hex frame>
  *   S <in_packets> <in_errors> <in_discards> <in_octets>
  *   Q <cos> <slot> <packets> <discards>     (odp_cls_queue_stats)
+ * RX_COUNT_ONLY=1: no P lines; "R <packets delivered> <ns>" (receive-path
+ *   rate, bench.py's runtime e2e: from odp_pktio_start to the last packet).
  */
 #define _GNU_SOURCE
 #include <inttypes.h>
@@ -71,7 +73,10 @@ static odp_pool_t mkpool(const char *name)
 	odp_pool_param_init(&p);
 	p.type = ODP_POOL_PACKET;
 	p.pkt.len = 1856;
-	p.pkt.seg_len = 1856;
+	/* RX_SEG_LEN: a first-segment length below the frame sizes (the
+	 * runtime still keeps every packet in one segment, seg_len being the
+	 * minimum the spec asks for) */
+	p.pkt.seg_len = getenv("RX_SEG_LEN") ? (uint32_t)atoi(getenv("RX_SEG_LEN")) : 1856;
 	p.pkt.num = 20000;
 	return odp_pool_create(name, &p);
 }
@@ -218,8 +223,15 @@ static void print_ev(const char *q, odp_event_t ev)
 	odp_event_free(ev);
 }
 
+static int count_only;
+static uint64_t delivered;
+
 static void print_pkt(const char *q, odp_packet_t pkt)
 {
+	if (count_only) {
+		delivered++;
+		return;
+	}
 	uint32_t len = odp_packet_len(pkt);
 	const uint8_t *d = odp_packet_data(pkt);
 	uint64_t fl = 0;
@@ -239,6 +251,8 @@ static void print_pkt(const char *q, odp_packet_t pkt)
 	/* checksum statuses (0 unknown, 1 bad, 2 ok) in bits 40-41 / 42-43 */
 	fl |= (uint64_t)odp_packet_l3_chksum_status(pkt) << 40;
 	fl |= (uint64_t)odp_packet_l4_chksum_status(pkt) << 42;
+	if (odp_packet_num_segs(pkt) != 1 || odp_packet_seg_len(pkt) != len)
+		printf("SEGMENTED %s\n", q);   /* never expected: tests fail on it */
 	printf("P %s %s %" PRIx64 " %d %u %u %" PRIu64 " %u ", q, poolname(odp_packet_pool(pkt)), fl,
 	       odp_packet_has_error(pkt), odp_packet_l3_offset(pkt), odp_packet_l4_offset(pkt),
 	       odp_packet_cls_mark(pkt), len);
@@ -334,6 +348,9 @@ int main(int argc, char *argv[])
 		replay(f, pktio, cos_pools);
 		fclose(f);
 	}
+	count_only = getenv("RX_COUNT_ONLY") != NULL;
+	odp_time_t t_start = odp_time_local();
+
 	if (odp_pktio_start(pktio))
 		return 8;
 
@@ -380,6 +397,17 @@ int main(int argc, char *argv[])
 				print_pkt("pktin", pk[i]);
 				odp_packet_free(pk[i]);
 			}
+			int m = 0;
+
+			if (count_only) {
+				/* rate runs: drain the CoS queues as the bursts come */
+				odp_event_t ev[256];
+				odp_queue_t from;
+
+				while ((m = odp_schedule_multi(&from, ODP_SCHED_NO_WAIT, ev, 256)) > 0)
+					for (int i = 0; i < m; i++)
+						print_ev("-", ev[i]);
+			}
 			idle = (n == 0 && odp_amd_pktio_rx_idle(pktio) == 1) ? idle + 1 : 0;
 		}
 		/* classified packets went to CoS queues: drain them */
@@ -418,6 +446,9 @@ int main(int argc, char *argv[])
 				usleep(2000);   /* let the aggregators' max_tmo_ns pass */
 		}
 	}
+	if (count_only)
+		printf("R %" PRIu64 " %" PRIu64 "\n", delivered,
+		       odp_time_diff_ns(odp_time_local(), t_start));
 	odp_pktio_stats_t st;
 
 	odp_pktio_stats(pktio, &st);

@@ -95,6 +95,7 @@ def run_driver(pktio, rules_path, mode="sched", layer=4, cos_pools=1, cls=1, src
         p = line.split()
         if not p:
             continue
+        assert p[0] != "SEGMENTED", line
         if p[0] in ("V", "E"):
             if events is not None:
                 events.setdefault(p[1], []).append((p[0], int(p[2])))

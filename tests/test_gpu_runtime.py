@@ -204,3 +204,32 @@ def test_rx_hash_queue_event_aggregators(built, gpu, tmp_path):
     for q in got[0]:
         if q not in hq:
             assert all(e == ("P",) for e in ev[q])
+
+
+def test_rx_small_first_segment(built, gpu, tmp_path):
+    """Pools whose pkt.seg_len (64 B) is below the frame sizes: the runtime
+    keeps every packet in one segment (seg_len is the minimum first-segment
+    length the spec asks for), so the parse sees seg_end = frame_len and the
+    reference's segmented-copy path (pktio/loop.c:299-306) has nothing to
+    do; rules on bytes deep in 1514-B frames (custom frame offset 1400)
+    classify as the oracle says, and every delivered packet is one segment."""
+    from odp_amd import pktgen as pg
+    frames = [f for _, f in zoo.all_frames()]
+    big = [pg.udp4_frame(src=f"10.0.0.{i}", dport=1000 + i, size=1514) for i in range(40)]
+    big = [f[:1400] + bytes([i & 0xFF, 0x5A]) + f[1402:] for i, f in enumerate(big)]
+    frames = H.pcap_frames(frames + big + frames)
+    prog = [R.cos("default", queue=1), R.cos("deep", queue=2), R.cos("v6", queue=3),
+            ("default", 0),
+            ("pmr", [R.t_custom(R.PMR_CUSTOM_FRAME, 1400, bytes([7, 0x5A]), b"\xff\xff")],
+             0, 1, 9),
+            ("pmr", [R.t_be16(R.PMR_ETHTYPE_0, pg.ETH_IPV6)], 0, 2, 0)]
+    pc = str(tmp_path / "in.pcap")
+    H.write_pcap(pc, frames)
+    rules = str(tmp_path / "rules.txt")
+    H.write_rules(rules, prog)
+    for pktio in ("pcap", "loop"):
+        env = {"RX_SEG_LEN": "64"}
+        got = (H.run_driver(f"pcap:in={pc}", rules, "sched", 4, 1, 1, env=env) if pktio == "pcap"
+               else H.run_driver("loop", rules, "sched", 4, 1, 1, src=pc, env=env))
+        H.compare(got, H.expected(prog, frames, 1, 1, 4))
+        assert len(got[0]["deep"]) == 1
