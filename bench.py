@@ -292,10 +292,12 @@ def time_runtime(batch, prog, n_frames=200_000, loops=10):
             if st:
                 v = [int(x) for x in st[-1].split()[1:5]]
                 out[mode].update(in_packets=v[0], in_errors=v[1], in_discards=v[2])
-    out["note"] = (f"ODP runtime receive path ({n} frames x {loops} loops of this workload's "
-                   f"traffic, pcap pktio, 4096-frame GPU bursts, CoS enqueue, one application "
+    out["note"] = (f"ODP runtime receive path, steady state after odp_pktio_start ({n} "
+                   f"frames x {loops} loops of this workload's traffic from a pcap pktio whose "
+                   f"page-locked frame store the GPU reads in place, 4096-frame bursts "
+                   f"pipelined two deep, packet alloc + copy + CoS enqueue, one application "
                    f"thread draining the queues): odp_pktin_recv (direct) and odp_schedule "
-                   f"(sched)")
+                   f"(sched); host-bound -- tools/rx_rate.sh splits the time per phase")
     return out
 
 

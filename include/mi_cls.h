@@ -186,14 +186,31 @@ int mi_cls_classify(mi_cls_ctx_t *ctx, const uint8_t *pkts_dev, const uint32_t *
 		    void *stream);
 
 /* Host-memory batch (the pktio receive path, loop.c:253-384 / pcap.c:280-401):
- * copies `bytes` of packed frames starting at pkts_host (offsets relative to
- * it) plus the descriptors to the context's device staging buffers on its own
- * stream, classifies, copies the n records to out_host and waits.  Host
- * buffers from mi_cls_host_alloc() (pinned) take the DMA fast path; any
- * other host memory is also accepted. */
+ * classifies n frames packed at pkts_host (offsets relative to it, every
+ * frame inside `bytes`), writes the n records to out_host and waits.
+ * When pkts_host, off_host, len_host and out_host are all page-locked
+ * (mi_cls_host_alloc, hipHostMalloc, hipHostRegister) the kernel reads the
+ * frames' header windows and the descriptors in place and writes the records
+ * in place (zero copy: only the bytes it touches cross the host link);
+ * otherwise the frames and descriptors are copied to the context's device
+ * staging buffers on its own stream and the records copied back. */
 int mi_cls_classify_host(mi_cls_ctx_t *ctx, const uint8_t *pkts_host, size_t bytes,
 			 const uint32_t *off_host, const uint16_t *len_host, uint32_t n,
 			 mi_cls_result_t *out_host);
+
+/* Pipelined form of mi_cls_classify_host: enqueue the batch on the context's
+ * stream and return a ticket (0 for n == 0); mi_cls_classify_host_wait(ticket)
+ * returns once its records are in out_host.  The caller leaves all four
+ * buffers untouched in between.  Up to 8 batches may be in flight; batches
+ * complete in submission order.  A rule load waits for the batches in
+ * flight, which classify under the rules they were submitted with.
+ * Replaces nothing in the reference (its receive burst parses
+ * synchronously, pktio/loop.c:253-384): it lets the runtime overlap one
+ * burst's classification with delivering the previous one. */
+int mi_cls_classify_host_submit(mi_cls_ctx_t *ctx, const uint8_t *pkts_host, size_t bytes,
+				const uint32_t *off_host, const uint16_t *len_host, uint32_t n,
+				mi_cls_result_t *out_host, uint64_t *ticket);
+int mi_cls_classify_host_wait(mi_cls_ctx_t *ctx, uint64_t ticket);
 
 /* ------------------------------------------------------------------------
  * Multi-GPU: one host batch over several devices.

@@ -294,6 +294,14 @@ int odp_amd_cls_classify_host(odp_pktio_t pktio, const uint8_t *pkts, size_t byt
 			      const uint32_t *off, const uint16_t *len, uint32_t n, void *out,
 			      int parse_only);
 
+/* Pipelined form (classifier enabled): submit a burst, wait for it later
+ * (mi_cls_classify_host_submit / _wait).  A multi-GPU pktio classifies the
+ * burst synchronously and returns ticket 0. */
+int odp_amd_cls_classify_host_submit(odp_pktio_t pktio, const uint8_t *pkts, size_t bytes,
+				     const uint32_t *off, const uint16_t *len, uint32_t n,
+				     void *out, uint64_t *ticket);
+int odp_amd_cls_classify_host_wait(odp_pktio_t pktio, uint64_t ticket);
+
 /* Create the device context, upload the current rule snapshot and run a
  * warm-up launch (odp_pktio_start). */
 int odp_amd_cls_prepare(odp_pktio_t pktio, int parse_only);

@@ -33,6 +33,10 @@ struct mi_cls_ctx {
 	uint16_t *d_len;
 	mi_cls_result_t *d_out;
 	uint32_t n_cap;
+	// submitted host batches (mi_cls_classify_host_submit): completion
+	// events in a ring, tickets numbered from 1
+	hipEvent_t ev[8];
+	uint64_t submitted;
 };
 
 #define HIP_OK(x) do { if ((x) != hipSuccess) return -EIO; } while (0)
@@ -91,8 +95,13 @@ extern "C" int mi_cls_ctx_destroy(mi_cls_ctx_t *c)
 		(void)hipFree(c->d_stats);
 	if (c->d_hint)
 		(void)hipFree(c->d_hint);
-	if (c->stream)
+	if (c->stream) {
+		(void)hipStreamSynchronize(c->stream);
 		(void)hipStreamDestroy(c->stream);
+	}
+	for (int i = 0; i < 8; ++i)
+		if (c->ev[i])
+			(void)hipEventDestroy(c->ev[i]);
 	(void)hipFree(c->d_pk);
 	(void)hipFree(c->d_off);
 	(void)hipFree(c->d_len);
@@ -860,6 +869,12 @@ extern "C" int mi_cls_rules_load(mi_cls_ctx_t *c, const void *tbl, size_t bytes,
 	rc = assemble(tbl, &w, &words);
 	if (rc)
 		return rc;
+	// host batches still in flight classify with the rules they were
+	// submitted under
+	if (c->stream && hipStreamSynchronize(c->stream) != hipSuccess) {
+		free(w);
+		return -EIO;
+	}
 	const uint32_t hot_words = w[DH_HOT_WORDS];
 	int tree = 0;
 	{
@@ -1058,14 +1073,43 @@ extern "C" int mi_cls_classify(mi_cls_ctx_t *c, const uint8_t *pkts, const uint3
 // records go to `out` (any host memory) or, when out is NULL, to the
 // context's pinned record buffer h_out (multi-GPU: no host wait per device).
 // Nothing is waited for here.
+// Device address of page-locked host memory (hipHostMalloc /
+// hipHostRegister), NULL for pageable memory.
+static const void *dev_view(const void *p)
+{
+	hipPointerAttribute_t a;
+	if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+		(void)hipGetLastError();
+		return nullptr;
+	}
+	if (a.type != hipMemoryTypeHost || !a.devicePointer || !a.hostPointer)
+		return nullptr;
+	return (const uint8_t *)a.devicePointer + ((const uint8_t *)p - (const uint8_t *)a.hostPointer);
+}
+
 static int host_launch(mi_cls_ctx_t *c, const uint8_t *pkts, size_t lo, size_t hi,
 		       const uint32_t *off, const uint16_t *len, uint32_t n, mi_cls_result_t *out)
 {
 	HIP_OK(hipSetDevice(c->device));
 	if (!c->stream)
 		HIP_OK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+	// Zero copy: frames and descriptors in page-locked memory are read by the
+	// kernel in place over the host link -- only the header windows it
+	// touches cross it, not whole frames -- and the records are written
+	// straight into page-locked `out`.
+	const void *zp = dev_view(pkts), *zo = zp ? dev_view(off) : nullptr;
+	const void *zl = zo ? dev_view(len) : nullptr;
+	if (zl) {
+		mi_cls_result_t *o = out ? out : n <= c->n_cap ? c->h_out : nullptr;
+		const void *zr = o ? dev_view(o) : nullptr;
+		if (zr)   // descriptors keep their offsets relative to `pkts`
+			return mi_cls_classify(c, (const uint8_t *)zp, (const uint32_t *)zo,
+					       (const uint16_t *)zl, n, (mi_cls_result_t *)zr, c->stream);
+	}
 	const size_t bytes = hi - lo;
 	const size_t need = bytes + 64;
+	if ((need > c->pk_cap || n > c->n_cap) && c->submitted)
+		HIP_OK(hipStreamSynchronize(c->stream));   // buffers of submitted batches
 	if (need > c->pk_cap) {
 		(void)hipFree(c->d_pk);
 		c->d_pk = nullptr;
@@ -1134,6 +1178,49 @@ extern "C" int mi_cls_classify_host(mi_cls_ctx_t *c, const uint8_t *pkts, size_t
 	if (rc)
 		return rc;
 	HIP_OK(hipStreamSynchronize(c->stream));
+	return 0;
+}
+
+// Submit a host batch without waiting (pipelined receive): the caller keeps
+// pkts / off / len / out untouched until mi_cls_classify_host_wait(ticket).
+extern "C" int mi_cls_classify_host_submit(mi_cls_ctx_t *c, const uint8_t *pkts, size_t bytes,
+					   const uint32_t *off, const uint16_t *len, uint32_t n,
+					   mi_cls_result_t *out, uint64_t *ticket)
+{
+	if (!c || !c->loaded || !ticket)
+		return -EINVAL;
+	*ticket = 0;
+	if (n == 0)
+		return 0;
+	if (!pkts || !off || !len || !out)
+		return -EINVAL;
+	for (uint32_t i = 0; i < n; ++i)
+		if ((size_t)off[i] + len[i] > bytes)
+			return -EINVAL;
+	const uint64_t t = c->submitted + 1;
+	hipEvent_t *ev = &c->ev[t % 8];
+	HIP_OK(hipSetDevice(c->device));
+	if (!*ev)
+		HIP_OK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
+	else
+		HIP_OK(hipEventSynchronize(*ev));   // ticket t - 8: done before its slot is reused
+	int rc = host_launch(c, pkts, 0, bytes, off, len, n, out);
+	if (rc)
+		return rc;
+	HIP_OK(hipEventRecord(*ev, c->stream));
+	c->submitted = t;
+	*ticket = t;
+	return 0;
+}
+
+extern "C" int mi_cls_classify_host_wait(mi_cls_ctx_t *c, uint64_t ticket)
+{
+	if (!c || ticket > c->submitted)
+		return -EINVAL;
+	if (ticket == 0 || ticket + 8 <= c->submitted)
+		return 0;   // nothing submitted, or its slot was reused (waited for then)
+	HIP_OK(hipSetDevice(c->device));
+	HIP_OK(hipEventSynchronize(c->ev[ticket % 8]));
 	return 0;
 }
 
@@ -1308,7 +1395,7 @@ extern "C" int mi_cls_pktin_opt_set(mi_cls_ctx_t *c, uint64_t opt)
 extern "C" void *mi_cls_host_alloc(size_t bytes)
 {
 	void *p = nullptr;
-	if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess)
+	if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocPortable | hipHostMallocMapped) != hipSuccess)
 		return nullptr;
 	return p;
 }

@@ -1380,6 +1380,43 @@ int odp_amd_cls_classify_host(odp_pktio_t h, const uint8_t *pkts, size_t bytes,
 	return mi_cls_classify_host(e->ctx, pkts, bytes, off, len, n, (mi_cls_result_t *)out);
 }
 
+int odp_amd_cls_classify_host_submit(odp_pktio_t h, const uint8_t *pkts, size_t bytes,
+				     const uint32_t *off, const uint16_t *len, uint32_t n,
+				     void *out, uint64_t *ticket)
+{
+	pktio_t *e = get_pktio(h);
+	int rc;
+
+	if (!e || !ticket)
+		return -EINVAL;
+	*ticket = 0;
+	rc = ensure_ctx(e);
+	if (rc)
+		return rc;
+	rc = sync_rules(e, NULL);
+	if (rc)
+		return rc;
+	if (e->grp) {
+		mi_cls_group_pktin_opt_set(e->grp, e->pktin_opt);
+		return mi_cls_group_classify_host(e->grp, pkts, bytes, off, len, n,
+						  (mi_cls_result_t *)out);
+	}
+	mi_cls_pktin_opt_set(e->ctx, e->pktin_opt);
+	return mi_cls_classify_host_submit(e->ctx, pkts, bytes, off, len, n,
+					   (mi_cls_result_t *)out, ticket);
+}
+
+int odp_amd_cls_classify_host_wait(odp_pktio_t h, uint64_t ticket)
+{
+	pktio_t *e = get_pktio(h);
+
+	if (!e)
+		return -EINVAL;
+	if (ticket == 0)
+		return 0;
+	return e->ctx ? mi_cls_classify_host_wait(e->ctx, ticket) : -EINVAL;
+}
+
 /* pktio start: device context, rule snapshot and a warm-up launch, so the
  * first received burst does not pay for GPU initialisation. */
 int odp_amd_cls_prepare(odp_pktio_t h, int parse_only)

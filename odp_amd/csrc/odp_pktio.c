@@ -35,15 +35,46 @@
 #include <stdlib.h>
 #include <string.h>
 #include <sys/time.h>
+#include <time.h>
 
 #include "odp_rt_internal.h"
 #include "mi_cls.h"
+
+static int rx_prof = -1;   /* ODP_AMD_RX_PROF set: receive-path phase times */
+
+static uint64_t prof_ns(void)
+{
+	struct timespec ts;
+
+	if (rx_prof <= 0)
+		return 0;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
 
 enum { DRV_LOOP = 1, DRV_PCAP, DRV_NULL };
 enum { ST_OPENED = 0, ST_STARTED, ST_STOPPED };
 
 #define RX_BURST_DEFAULT 4096
 #define PCAP_MTU_MAX (64 * 1024)
+
+/* One receive burst on its way through the GPU. */
+typedef struct {
+	uint8_t *stage;         /* copies of the frames (64 B aligned offsets) */
+	size_t stage_cap;
+	int stage_pinned;
+	const uint8_t *base;    /* the burst's frames: base + soff[i], slen[i] bytes */
+	size_t bytes;
+	uint32_t *soff;
+	uint16_t *slen;
+	mi_cls_result_t *res;
+	odp_packet_t *pk;       /* loop driver: the packets themselves */
+	uint32_t n_cap;
+	int arr_pinned;
+	int n;
+	int pending;            /* staged (and submitted), not delivered */
+	uint64_t ticket;        /* odp_amd_cls_classify_host_submit, 0 = done */
+} rx_set_t;
 
 typedef struct {
 	int used;
@@ -73,18 +104,18 @@ typedef struct {
 	FILE *tx;
 	/* loop */
 	odp_queue_t loopq;
-	/* staging for the GPU burst */
-	uint8_t *stage;
-	int stage_pinned;
-	size_t stage_cap;
-	uint32_t *soff;
-	uint16_t *slen;
-	mi_cls_result_t *res;
-	odp_packet_t *pk;
-	uint32_t n_cap;
+	size_t fbuf_bytes;      /* frame store size incl. 64 B of zero padding */
+	int fbuf_pinned;        /* page-locked: the GPU reads frames in place */
+	/* GPU bursts: two staging sets, so one burst is classified while the
+	 * previous one is delivered (pipelined receive) */
+	rx_set_t rs[2];
+	int cur;                /* set the next burst is staged into */
+	uint64_t prof[4];       /* ODP_AMD_RX_PROF: ns staging / classifying / delivering, bursts */
 } rt_pktio_t;
 
-static void stage_free(rt_pktio_t *e);
+static void rx_sets_free(rt_pktio_t *e);
+static void fbuf_free(rt_pktio_t *e);
+static int rx_finish(rt_pktio_t *e, rx_set_t *s, odp_packet_t out[], int max_out);
 
 static rt_pktio_t PK[RT_MAX_PKTIO];
 static odp_spinlock_t pk_lock;
@@ -286,6 +317,22 @@ bad_link:
 bad:
 	RT_ERR("%s: not a pcap / pcapng file\n", fname);
 out:
+	if (rc == 0 && e->fbuf) {
+		/* page-locked frame store: the GPU reads the bursts' header windows
+		 * in place (zero copy, mi_cls_classify_host) and no staging copy is
+		 * made.  ODP_AMD_RX_INPLACE=0 keeps the staged copies (A/B runs). */
+		const char *v = getenv("ODP_AMD_RX_INPLACE");
+		uint8_t *pb = v && v[0] == '0' ? NULL : mi_cls_host_alloc(used_b + 64);
+
+		e->fbuf_bytes = used_b + 64;
+		if (pb) {
+			memcpy(pb, e->fbuf, used_b);
+			memset(pb + used_b, 0, 64);
+			free(e->fbuf);
+			e->fbuf = pb;
+			e->fbuf_pinned = 1;
+		}
+	}
 	free(buf);
 	fclose(f);
 	return rc;
@@ -464,7 +511,7 @@ odp_pktio_t odp_pktio_open(const char *name, odp_pool_t pool, const odp_pktio_pa
 	e->state = ST_OPENED;
 	e->promisc = 1;
 	if (drv == DRV_PCAP && pcap_open(e, name)) {
-		free(e->fbuf);
+		fbuf_free(e);
 		free(e->foff);
 		free(e->flen);
 		e->used = 0;
@@ -712,6 +759,10 @@ int odp_pktio_stop(odp_pktio_t h)
 	}
 	sched_list_remove((int)((uintptr_t)h - 1));
 	odp_spinlock_lock(&e->rxl);   /* wait for an in-flight burst */
+	/* a burst still on the GPU was received before the stop: deliver it */
+	for (int k = 0; k < 2; k++)
+		if (e->rs[e->cur ^ 1 ^ k].pending)
+			(void)rx_finish(e, &e->rs[e->cur ^ 1 ^ k], NULL, 0);
 	e->state = ST_STOPPED;
 	odp_spinlock_unlock(&e->rxl);
 	return 0;
@@ -727,6 +778,10 @@ int odp_pktio_close(odp_pktio_t h)
 		RT_ERR("pktio %s: close while started\n", e->name);
 		return -1;
 	}
+	if (rx_prof > 0 && e->prof[3])
+		fprintf(stderr, "RXPROF %s bursts %" PRIu64 " stage_ns %" PRIu64 " classify_ns %" PRIu64
+			" deliver_ns %" PRIu64 "\n", e->name, e->prof[3], e->prof[0], e->prof[1],
+			e->prof[2]);
 	if (e->inq != ODP_QUEUE_INVALID) {
 		odp_event_t ev[64];
 		int n;
@@ -745,14 +800,10 @@ int odp_pktio_close(odp_pktio_t h)
 	}
 	if (e->tx)
 		fclose(e->tx);
-	free(e->fbuf);
+	fbuf_free(e);
 	free(e->foff);
 	free(e->flen);
-	stage_free(e);
-	free(e->soff);
-	free(e->slen);
-	free(e->res);
-	free(e->pk);
+	rx_sets_free(e);
 	odp_spinlock_lock(&pk_lock);
 	memset(e, 0, sizeof(*e));
 	odp_spinlock_unlock(&pk_lock);
@@ -760,58 +811,100 @@ int odp_pktio_close(odp_pktio_t h)
 }
 
 /* ============================================================ receive */
-static void stage_free(rt_pktio_t *e)
+/* Host memory the GPU can read in place (page-locked) where there is a GPU,
+ * ordinary memory otherwise (parse layer NONE needs none). */
+static void *hmem_alloc(size_t bytes, int *pinned)
 {
-	if (e->stage_pinned)
-		mi_cls_host_free(e->stage);
+	void *p = mi_cls_host_alloc(bytes);
+
+	*pinned = p != NULL;
+	return p ? p : malloc(bytes);
+}
+
+static void hmem_free(void *p, int pinned)
+{
+	if (pinned)
+		mi_cls_host_free(p);
 	else
-		free(e->stage);
-	e->stage = NULL;
+		free(p);
+}
+
+static void fbuf_free(rt_pktio_t *e)
+{
+	hmem_free(e->fbuf, e->fbuf_pinned);
+	e->fbuf = NULL;
+	e->fbuf_pinned = 0;
+}
+
+static void rx_set_arrays_free(rx_set_t *s)
+{
+	hmem_free(s->soff, s->arr_pinned);
+	hmem_free(s->slen, s->arr_pinned);
+	hmem_free(s->res, s->arr_pinned);
+	free(s->pk);
+	s->soff = NULL;
+	s->slen = NULL;
+	s->res = NULL;
+	s->pk = NULL;
+	s->n_cap = 0;
+}
+
+static void rx_sets_free(rt_pktio_t *e)
+{
+	for (int k = 0; k < 2; k++) {
+		rx_set_t *s = &e->rs[k];
+
+		hmem_free(s->stage, s->stage_pinned);
+		rx_set_arrays_free(s);
+		memset(s, 0, sizeof(*s));
+	}
 }
 
 /* descriptor arrays for n frames; stage bytes grow keeping the contents */
-static int stage_reserve(rt_pktio_t *e, uint32_t n, size_t bytes)
+static int stage_reserve(rx_set_t *s, uint32_t n, size_t bytes)
 {
-	if (n > e->n_cap) {
+	if (n > s->n_cap) {
 		uint32_t c = n < 256 ? 256 : n;
+		int p1, p2, p3;
 
-		free(e->soff);
-		free(e->slen);
-		free(e->res);
-		free(e->pk);
-		e->soff = malloc(c * sizeof(uint32_t));
-		e->slen = malloc(c * sizeof(uint16_t));
-		e->res = malloc(c * sizeof(mi_cls_result_t));
-		e->pk = malloc(c * sizeof(odp_packet_t));
-		if (!e->soff || !e->slen || !e->res || !e->pk) {
-			e->n_cap = 0;
+		rx_set_arrays_free(s);
+		s->soff = hmem_alloc(c * sizeof(uint32_t), &p1);
+		s->slen = hmem_alloc(c * sizeof(uint16_t), &p2);
+		s->res = hmem_alloc(c * sizeof(mi_cls_result_t), &p3);
+		s->arr_pinned = p1;
+		s->pk = malloc(c * sizeof(odp_packet_t));
+		if (p1 != p2 || p1 != p3) {   /* mixed: keep the pageable copies */
+			hmem_free(s->soff, p1);
+			hmem_free(s->slen, p2);
+			hmem_free(s->res, p3);
+			s->soff = malloc(c * sizeof(uint32_t));
+			s->slen = malloc(c * sizeof(uint16_t));
+			s->res = malloc(c * sizeof(mi_cls_result_t));
+			s->arr_pinned = 0;
+		}
+		if (!s->soff || !s->slen || !s->res || !s->pk) {
+			rx_set_arrays_free(s);
 			return -1;
 		}
-		e->n_cap = c;
+		s->n_cap = c;
 	}
-	if (bytes > e->stage_cap) {
-		size_t c = e->stage_cap ? e->stage_cap : (4u << 20);
+	if (bytes > s->stage_cap) {
+		size_t c = s->stage_cap ? s->stage_cap : (4u << 20);
+		int pinned;
 
 		while (c < bytes)
 			c *= 2;
-		/* pinned memory takes the DMA-direct H2D path; without a GPU
-		 * (parse layer NONE) pageable memory serves */
-		int pinned = 1;
-		uint8_t *ns = mi_cls_host_alloc(c);
+		uint8_t *ns = hmem_alloc(c, &pinned);
 
-		if (!ns) {
-			ns = malloc(c);
-			pinned = 0;
-		}
 		if (!ns)
 			return -1;
-		if (e->stage) {
-			memcpy(ns, e->stage, e->stage_cap);
-			stage_free(e);
+		if (s->stage) {
+			memcpy(ns, s->stage, s->stage_cap);
+			hmem_free(s->stage, s->stage_pinned);
 		}
-		e->stage = ns;
-		e->stage_pinned = pinned;
-		e->stage_cap = c;
+		s->stage = ns;
+		s->stage_pinned = pinned;
+		s->stage_cap = c;
 	}
 	return 0;
 }
@@ -953,17 +1046,25 @@ static void cos_enq_run(odp_packet_t pk[], int num)
 	cos_vector_enq(dst, pk, num, cos, vpool, vmax);
 }
 
-/* Pull up to `max` frames from the driver into the staging buffer (64 B
- * aligned offsets).  Loop frames keep their packets in e->pk; pcap frames are
- * allocated later, directly from the final pool.  Returns the frame count. */
-static int stage_frames(rt_pktio_t *e, uint32_t max, size_t *bytes)
+/* Pull up to `max` frames from the driver into staging set s.  pcap frames
+ * in a page-locked frame store are not copied: the set points at the store
+ * (the GPU reads them there) and they are copied once, into their packets,
+ * at delivery.  Other pcap frames are copied into the stage (64 B aligned
+ * offsets) and allocated later, directly from the final pool; loop frames
+ * keep their packets in s->pk.  Returns the frame count. */
+static int stage_frames(rt_pktio_t *e, rx_set_t *s, uint32_t max)
 {
 	uint32_t n = 0;
 	size_t off = 0;
 
-	if (stage_reserve(e, max, 0))
+	if (stage_reserve(s, max, 0))
 		return -1;
+	s->base = s->stage;
 	if (e->drv == DRV_PCAP) {
+		const int in_place = e->fbuf_pinned;
+
+		if (in_place)
+			s->base = e->fbuf;
 		while (n < max) {
 			if (e->next >= e->nframes) {
 				if (e->nframes == 0 || e->eof)
@@ -975,20 +1076,27 @@ static int stage_frames(rt_pktio_t *e, uint32_t max, size_t *bytes)
 				}
 				e->next = 0;
 			}
-			const uint8_t *d = e->fbuf + e->foff[e->next];
+			const uint32_t fo = e->foff[e->next];
+			const uint8_t *d = e->fbuf + fo;
 			uint16_t l = e->flen[e->next];
 
 			e->next++;
 			if (!pcap_filter_pass(e, d, l))
 				continue;
-			if (stage_reserve(e, max, off + l + 64))
-				return -1;
-			memcpy(e->stage + off, d, l);
-			e->soff[n] = (uint32_t)off;
-			e->slen[n] = l;
-			off += ((uint32_t)l + 63u) & ~63u;
+			if (in_place) {
+				s->soff[n] = fo;
+			} else {
+				if (stage_reserve(s, max, off + l + 64))
+					return -1;
+				s->base = s->stage;
+				memcpy(s->stage + off, d, l);
+				s->soff[n] = (uint32_t)off;
+				off += ((uint32_t)l + 63u) & ~63u;
+			}
+			s->slen[n] = l;
 			n++;
 		}
+		s->bytes = in_place ? e->fbuf_bytes : off + 64;
 	} else if (e->drv == DRV_LOOP) {
 		odp_event_t ev[256];
 
@@ -1003,65 +1111,124 @@ static int stage_frames(rt_pktio_t *e, uint32_t max, size_t *bytes)
 				pkt_hdr_t *h = rt_pkt_hdr(p);
 				uint32_t l = h->len > 65535 ? 65535 : h->len;
 
-				if (stage_reserve(e, max, off + l + 64)) {
+				if (stage_reserve(s, max, off + l + 64)) {
 					odp_event_free_multi(&ev[i], got - i);
-					odp_packet_free_multi(e->pk, (int)n);
+					odp_packet_free_multi(s->pk, (int)n);
 					return -1;
 				}
-				memcpy(e->stage + off, h->head + h->data_off, l);
-				e->soff[n] = (uint32_t)off;
-				e->slen[n] = (uint16_t)l;
-				e->pk[n] = p;
+				memcpy(s->stage + off, h->head + h->data_off, l);
+				s->soff[n] = (uint32_t)off;
+				s->slen[n] = (uint16_t)l;
+				s->pk[n] = p;
 				off += (l + 63u) & ~63u;
 				n++;
 			}
 			if (got < want)
 				break;
 		}
+		s->base = s->stage;
+		s->bytes = off + 64;
 	}
-	*bytes = off + 64;
 	return (int)n;
 }
 
-/* One receive burst.  Unclassified packets are returned in out[] (at most
- * max_out); classified ones are enqueued to their CoS queues. */
-static int pktio_recv(rt_pktio_t *e, odp_packet_t out[], int max_out)
+/* more frames ready at the driver right now (a burst in flight can wait) */
+static int rx_more(rt_pktio_t *e)
 {
-	size_t bytes = 0;
-	uint32_t burst = rx_burst();
+	if (e->drv == DRV_PCAP)
+		return e->nframes && !e->eof &&
+		       (e->next < e->nframes || e->loops == 0 || e->loop_cnt + 1 < e->loops);
+	if (e->drv == DRV_LOOP)
+		return ((rt_queue_t *)(void *)e->loopq)->count > 0;
+	return 0;
+}
 
-	if (!e->cls_enabled && (uint32_t)max_out < burst)
-		burst = (uint32_t)max_out;
-	int n = stage_frames(e, burst, &bytes);
+/* ODP_AMD_RX_PIPELINE=0: classify each burst synchronously */
+static int rx_pipeline(void)
+{
+	static int on = -1;
 
-	if (n <= 0)
-		return n;
+	if (on < 0) {
+		const char *v = getenv("ODP_AMD_RX_PIPELINE");
+
+		on = !(v && v[0] == '0');
+	}
+	return on;
+}
+
+static void rx_drop(rt_pktio_t *e, rx_set_t *s, int rc)
+{
+	RT_ERR("pktio %s: GPU classify failed (%s), burst of %d dropped\n", e->name,
+	       mi_cls_strerror(rc), s->n);
+	if (e->drv == DRV_LOOP)
+		odp_packet_free_multi(s->pk, s->n);
+	odp_atomic_add_u64(&e->in_discards, (uint64_t)s->n);
+	s->pending = 0;
+}
+
+/* Classify set s: submitted to the GPU (pipelined) or done on return.  On
+ * failure the burst is dropped and counted; returns 0 / -1. */
+static int rx_classify(rt_pktio_t *e, rx_set_t *s, int pipe)
+{
+	int rc = 0;
+
+	s->ticket = 0;
+	s->pending = 1;
+	if (e->parse_layer == ODP_PROTO_LAYER_NONE)
+		return 0;
+	if (pipe)
+		rc = odp_amd_cls_classify_host_submit(e->hdl, s->base, s->bytes, s->soff, s->slen,
+						      (uint32_t)s->n, s->res, &s->ticket);
+	else
+		rc = odp_amd_cls_classify_host(e->hdl, s->base, s->bytes, s->soff, s->slen,
+					       (uint32_t)s->n, s->res, !e->cls_enabled);
+	if (rc) {
+		rx_drop(e, s, rc);
+		return -1;
+	}
+	return 0;
+}
+
+/* Wait for set s's records and deliver its packets: classified ones to their
+ * CoS queues, the rest (classifier disabled) into out[] (at most max_out).
+ * Returns the packets placed in out[]. */
+static int rx_finish(rt_pktio_t *e, rx_set_t *s, odp_packet_t out[], int max_out)
+{
 	const odp_proto_layer_t layer = e->parse_layer;
+	uint64_t t1 = prof_ns();
 
-	if (layer != ODP_PROTO_LAYER_NONE) {
-		int rc = odp_amd_cls_classify_host(e->hdl, e->stage, bytes, e->soff, e->slen,
-						   (uint32_t)n, e->res, !e->cls_enabled);
+	if (s->ticket) {
+		int rc = odp_amd_cls_classify_host_wait(e->hdl, s->ticket);
 
+		s->ticket = 0;
 		if (rc) {
-			RT_ERR("pktio %s: GPU classify failed (%s), burst of %d dropped\n", e->name,
-			       mi_cls_strerror(rc), n);
-			if (e->drv == DRV_LOOP)
-				odp_packet_free_multi(e->pk, n);
-			odp_atomic_add_u64(&e->in_discards, (uint64_t)n);
+			rx_drop(e, s, rc);
 			return 0;
 		}
 	}
-	odp_packet_t *run = e->pk;   /* reused in place: run[j] <= pk[i], j <= i */
+	uint64_t t2 = prof_ns();
+
+	e->prof[1] += t2 - t1;
+	s->pending = 0;
+	odp_packet_t *run = s->pk;   /* reused in place: run[j] <= pk[i], j <= i */
 	int nrun = 0, num_rx = 0;
 	uint64_t octets = 0, packets = 0;
 
-	for (int i = 0; i < n; i++) {
+	for (int i = 0; i < s->n; i++) {
 		mi_cls_result_t r;
-		odp_packet_t pkt = e->drv == DRV_LOOP ? e->pk[i] : ODP_PACKET_INVALID;
-		uint32_t len = e->slen[i];
+		odp_packet_t pkt = e->drv == DRV_LOOP ? s->pk[i] : ODP_PACKET_INVALID;
+		uint32_t len = s->slen[i];
+
+		if (i + 8 < s->n) {   /* frames read in place are cold in the CPU caches */
+			const uint8_t *nf = s->base + s->soff[i + 8];
+			const uint32_t nl = s->slen[i + 8];
+
+			for (uint32_t b = 0; b < nl; b += 64)
+				__builtin_prefetch(nf + b);
+		}
 
 		if (layer != ODP_PROTO_LAYER_NONE) {
-			r = e->res[i];
+			r = s->res[i];
 			apply_layer(&r, layer);
 			if (r.err || r.outcome == MI_CLS_OUT_PARSE_DROP)
 				odp_atomic_inc_u64(&e->in_errors);
@@ -1095,7 +1262,7 @@ static int pktio_recv(rt_pktio_t *e, odp_packet_t out[], int max_out)
 					odp_atomic_inc_u64(&e->in_discards);
 				continue;
 			}
-			memcpy(odp_packet_data(pkt), e->stage + e->soff[i], len);
+			memcpy(odp_packet_data(pkt), s->base + s->soff[i], len);
 		} else if (odp_packet_pool(pkt) != pool) {
 			odp_packet_t np = odp_packet_alloc(pool, len);
 
@@ -1150,8 +1317,52 @@ static int pktio_recv(rt_pktio_t *e, odp_packet_t out[], int max_out)
 	}
 	if (nrun)
 		cos_enq_run(run, nrun);
+	e->prof[2] += prof_ns() - t2;
 	odp_atomic_add_u64(&e->in_octets, octets);
 	odp_atomic_add_u64(&e->in_packets, packets);
+	return num_rx;
+}
+
+/* One receive call.  With the classifier enabled, a burst whose successor is
+ * already waiting at the driver is left in flight on the GPU while the
+ * previous burst is delivered (one burst of latency, none when the driver
+ * has nothing more: a call always delivers everything that was ready).
+ * Unclassified packets are returned in out[] (at most max_out); classified
+ * ones are enqueued to their CoS queues. */
+static int pktio_recv(rt_pktio_t *e, odp_packet_t out[], int max_out)
+{
+	rx_set_t *s = &e->rs[e->cur], *p = &e->rs[e->cur ^ 1];
+	const int pipe = e->cls_enabled && e->parse_layer != ODP_PROTO_LAYER_NONE &&
+			 rx_pipeline();
+	uint32_t burst = rx_burst();
+	int num_rx = 0;
+
+	if (rx_prof < 0)
+		rx_prof = getenv("ODP_AMD_RX_PROF") != NULL;
+	if (!e->cls_enabled && (uint32_t)max_out < burst)
+		burst = (uint32_t)max_out;
+	uint64_t t0 = prof_ns();
+	int n = stage_frames(e, s, burst);
+	uint64_t t1 = prof_ns();
+
+	e->prof[0] += t1 - t0;
+	if (n < 0 && !p->pending)
+		return n;
+	s->n = n > 0 ? n : 0;
+	if (n > 0) {
+		e->prof[3]++;
+		if (rx_classify(e, s, pipe))
+			n = 0;
+		e->prof[1] += prof_ns() - t1;
+	}
+	if (p->pending)
+		num_rx += rx_finish(e, p, out, max_out);
+	if (n > 0) {
+		if (pipe && rx_more(e))
+			e->cur ^= 1;   /* s stays in flight: the next call stages into p */
+		else
+			num_rx += rx_finish(e, s, out + num_rx, max_out - num_rx);
+	}
 	return num_rx;
 }
 
@@ -1391,7 +1602,9 @@ int odp_amd_pktio_rx_idle(odp_pktio_t h)
 	if (!e)
 		return -1;
 	odp_spinlock_lock(&e->rxl);
-	if (e->drv == DRV_PCAP)
+	if (e->rs[0].pending || e->rs[1].pending)
+		idle = 0;
+	else if (e->drv == DRV_PCAP)
 		idle = e->eof || e->nframes == 0 || (e->next >= e->nframes && e->loops == 1);
 	else if (e->drv == DRV_LOOP)
 		idle = ((rt_queue_t *)(void *)e->loopq)->count == 0;

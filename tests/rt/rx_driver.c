@@ -349,10 +349,11 @@ int main(int argc, char *argv[])
 		fclose(f);
 	}
 	count_only = getenv("RX_COUNT_ONLY") != NULL;
-	odp_time_t t_start = odp_time_local();
-
 	if (odp_pktio_start(pktio))
 		return 8;
+	/* rate runs time the steady state: GPU context, rule upload and the
+	 * warm-up launch happen in odp_pktio_start */
+	odp_time_t t_start = odp_time_local();
 
 	/* loop: feed the source frames through a parse-less pcap pktio */
 	if (strncmp(argv[1], "loop", 4) == 0 && argc > 7) {

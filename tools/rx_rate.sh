@@ -1,0 +1,28 @@
+#!/bin/bash
+# Runtime receive rates on config 3 traffic with the per-phase profile;
+# A/B: synchronous bursts (ODP_AMD_RX_PIPELINE=0), staged copies
+# (ODP_AMD_RX_INPLACE=0).  Usage: tools/rx_rate.sh OUTDIR [frames] [loops]
+set -o pipefail
+OUT=${1:-gpurun_out/rx}
+mkdir -p $OUT
+timeout -k 10 120 python - "$OUT" ${2:-200000} <<'PY' || exit 1
+import sys
+sys.path.insert(0, ".")
+from odp_amd import rules as R
+from tests import rt_helpers as H
+b, p = R.config3(int(sys.argv[2]))
+H.write_pcap(sys.argv[1] + "/in.pcap", [b.frame(i) for i in range(b.n)])
+H.write_rules(sys.argv[1] + "/rules.txt", p)
+PY
+run() {  # name mode env...
+  local name=$1 m=$2; shift 2
+  env "$@" ODP_AMD_RX_PROF=1 RX_COUNT_ONLY=1 timeout -k 10 120 tests/_bin/rx_driver pcap:in=$OUT/in.pcap:loops=${LOOPS:-10} $OUT/rules.txt $m 4 0 1 > $OUT/$name.txt 2>&1 || { tail $OUT/$name.txt; exit 1; }
+  echo "$name: $(grep -E '^(R|S|RXPROF) ' $OUT/$name.txt | sed 's/pcap:in=[^ ]* //' | tr '\n' ' ')"
+}
+LOOPS=${3:-10}
+run direct direct NONE=1
+run sched sched NONE=1
+run direct_sync direct ODP_AMD_RX_PIPELINE=0
+run direct_staged direct ODP_AMD_RX_INPLACE=0
+run direct_sync_staged direct ODP_AMD_RX_PIPELINE=0 ODP_AMD_RX_INPLACE=0
+rm -f $OUT/in.pcap
