@@ -47,7 +47,8 @@ HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 N_SIMD = 256 * 4           # 256 CUs x 4 SIMDs
 SCLK_GHZ = 2.4             # peak engine clock
 WORKLOAD = {2: "config2", 3: "config3", 4: "config4", 5: "config5", 33: "config3_64B",
-            1: "config1", 20: "config2_norules", 34: "config3_64rules"}
+            1: "config1", 20: "config2_norules", 34: "config3_64rules",
+            35: "config3_sctp"}
 
 
 def parse_args():
@@ -65,6 +66,9 @@ def parse_args():
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--timed-only", action="store_true",
                     help="only the timed single-config pass (profiling runs)")
+    ap.add_argument("--pktin-opt", type=lambda x: int(x, 0), default=0,
+                    help="pktin checksum/drop option bits for the main line (profiling the "
+                         "checksum path: 0x3C); valid checksums are written into the batch")
     ap.add_argument("--streams", type=int, default=1,
                     help="HIP streams the timed launches alternate over (1: back to back)")
     ap.add_argument("--rotate", type=int, default=4,
@@ -93,6 +97,8 @@ def make_workload(cfg, n, rank):
         return b, [op for op in p if op[0] != "pmr"]
     if cfg == 34:   # config 3 IMIX traffic, 64 rules
         return R.config3(n, num_rules=64, rank=rank)
+    if cfg == 35:   # config 3 IMIX traffic with a third of the packets SCTP
+        return R.config3(n, rank=rank, sctp_frac=1.0 / 3.0)
     raise ValueError(cfg)
 
 
@@ -169,11 +175,11 @@ def records(t_out, n):
     return t_out.cpu().numpy().view(np.uint8).reshape(-1)[: 16 * n].view(R.RESULT_DTYPE)
 
 
-def oracle_parity(prog, batch, got, threads=16):
+def oracle_parity(prog, batch, got, threads=16, pktin_opt=0):
     """Bit-exact check of every record against the oracle (multi-threaded)."""
     import numpy as np
     from oracle.oracle import Oracle
-    o = Oracle()
+    o = Oracle(pktin_opt=pktin_opt)
     o.apply(prog)
     exp = o.classify(batch, threads=threads)
     return bool(np.array_equal(got, exp))
@@ -441,6 +447,10 @@ def main():
     batch, prog = make_workload(a.config, n_rank, rank)
     c = cls.Classifier(gpu=local)
     c.apply(prog)
+    if a.pktin_opt:
+        from odp_amd import pktgen as pg
+        pg.set_checksums(batch)
+        c.set_pktin_opt(a.pktin_opt)
 
     wall, kms, t_out = time_device(c, batch, dev, a.steps, a.warmup, dist_on, a.rotate,
                                    a.streams)
@@ -456,7 +466,9 @@ def main():
     else:
         total_pkts = batch.n * a.steps
     value = total_pkts / wall / 1e6
-    bytes_launch = batch.header_bytes()
+    # with checksum options the kernel reads every frame byte
+    bytes_launch = batch.header_bytes() if not a.pktin_opt else \
+        int(batch.len.astype("int64").sum()) + 22 * batch.n
     achieved = bytes_launch / (kms * 1e-3) / 1e9
     res = None
     if rank == 0:
@@ -491,7 +503,7 @@ def main():
         }
         if not a.no_parity and not a.timed_only:
             # this rank's records, every one bit-exact vs the oracle
-            line["parity_vs_oracle"] = oracle_parity(prog, batch, out)
+            line["parity_vs_oracle"] = oracle_parity(prog, batch, out, pktin_opt=a.pktin_opt)
         if world == 1 and not a.timed_only:
             if R.rule_count(prog) >= 256:
                 line["compute"] = compute_roof(prog, batch, kms, pmc)
@@ -522,6 +534,11 @@ def main():
                 extra["config3_checksums"] = bench_cfg(cls, 3, a, dev, local, k_steps, 3,
                                                        pktin_opt=0x3C, parity=not a.no_parity,
                                                        full_bytes=True)
+                # the same with a third of the packets SCTP (CRC-32C over the
+                # whole frame, slicing-by-4 per lane)
+                extra["config3_sctp_checksums"] = bench_cfg(cls, 35, a, dev, local, k_steps, 3,
+                                                            pktin_opt=0x3C, parity=not a.no_parity,
+                                                            full_bytes=True)
                 line["extra"] = extra
         res = line
         print(json.dumps(res), flush=True)

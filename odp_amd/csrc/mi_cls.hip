@@ -1023,6 +1023,14 @@ extern "C" int mi_cls_classify(mi_cls_ctx_t *c, const uint8_t *pkts, const uint3
 		if (nw != 4 && nw != 16 && !lt)
 			nw = 16;   // 8 / 12-wave blocks exist for LDS-resident hot regions only
 	}
+	if (c->opt != 0 && nw != 4) {
+		// the pktin-option kernels exist as 4-wave blocks and as 16-wave
+		// blocks with the hot region in LDS
+		nw = 16;
+		lt = st_of(16) + hot_bytes <= LDS_CU;
+		if (!lt)
+			nw = 4;
+	}
 	const size_t lds_block = st_of(nw) + (lt ? hot_bytes : 0);
 	const bool div = c->tree;
 	int per_cu = (int)(LDS_CU / lds_block);
@@ -1040,7 +1048,9 @@ extern "C" int mi_cls_classify(mi_cls_ctx_t *c, const uint8_t *pkts, const uint3
 	const size_t dyn = lt ? hot_bytes : 0;
 	hipStream_t st = (hipStream_t)stream;
 	int lrc;
-	if (c->flat_mode >= 0 && c->opt == 0 && lt && (nw == 4 || nw == 12 || nw == 16))
+	if (c->opt != 0)
+		lrc = mi_cls_launch_ck(nw, lt, div, grid, dyn, st, a);
+	else if (c->flat_mode >= 0 && lt && (nw == 4 || nw == 12 || nw == 16))
 		lrc = mi_cls_launch_flat(nw, c->flat_mode, grid, dyn, st, a);
 	else if (nw == 16)
 		lrc = mi_cls_launch_k16(lt, div, grid, dyn, st, a);

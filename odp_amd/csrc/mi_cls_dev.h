@@ -405,100 +405,219 @@ __device__ __forceinline__ Parsed parse_packet(const Pkt &k, uint32_t opt)
 }
 
 // ------------------------------------------------------- pktin checksums
-// CRC-32C (Castagnoli, reflected polynomial 0x82F63B78) byte table, the
-// arithmetic of odp_hash_crc32c (arch/default/odp_hash_crc32.c: table-driven,
-// caller-supplied init, no final inversion).
+// Buffer offset no frame byte reaches: num_records of the packet resource, so
+// a load at or past it returns zeros (batches are < 4 GiB: u32 offsets).
+#define OOB_OFF 0xFFFFFE00u
+
+// CRC-32C (Castagnoli, reflected polynomial 0x82F63B78), the arithmetic of
+// odp_hash_crc32c (arch/default/odp_hash_crc32.c: table-driven,
+// caller-supplied init, no final inversion), as slicing-by-4 tables: t[0] is
+// the byte table, t[k][i] = t[k-1][i] >> 8 ^ t[0][t[k-1][i] & 0xff], so four
+// bytes advance with four independent lookups instead of four dependent ones.
 struct Crc32cTab {
-	uint32_t v[256];
-	constexpr Crc32cTab() : v()
+	uint32_t t[4][256];
+	constexpr Crc32cTab() : t()
 	{
 		for (uint32_t i = 0; i < 256; ++i) {
 			uint32_t c = i;
 			for (int b = 0; b < 8; ++b)
 				c = (c & 1u) ? (c >> 1) ^ 0x82F63B78u : (c >> 1);
-			v[i] = c;
+			t[0][i] = c;
 		}
+		for (int k = 1; k < 4; ++k)
+			for (uint32_t i = 0; i < 256; ++i)
+				t[k][i] = (t[k - 1][i] >> 8) ^ t[0][t[k - 1][i] & 0xffu];
 	}
 };
 static __constant__ Crc32cTab c_crc32c;
 
 __device__ __forceinline__ uint32_t crc32c_u8(uint32_t crc, uint32_t b)
 {
-	return c_crc32c.v[(crc ^ b) & 0xffu] ^ (crc >> 8);
+	return c_crc32c.t[0][(crc ^ b) & 0xffu] ^ (crc >> 8);
 }
 
-// Sum of the little-endian 32-bit words of frame bytes [from, to) (bytes
-// outside are masked to zero), read from HBM in 16-B pieces that start on
-// frame-relative 16-B boundaries, so no piece reaches past the next 16-B
-// boundary after the frame (the batch contract, mi_cls.h).  `from` is even:
-// every 16-bit word of the one's-complement sum stays in one half of a dword.
-__device__ __forceinline__ uint64_t ck_sum_frame(__amdgpu_buffer_rsrc_t rs, uint32_t boff,
-						  uint32_t from, uint32_t to)
+// four bytes, little-endian word w (byte 0 first on the wire)
+__device__ __forceinline__ uint32_t crc32c_u32(uint32_t crc, uint32_t w)
 {
-	uint64_t s = 0;
-	for (uint32_t p = from & ~15u; p < to; p += 16u) {
-		const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, boff + p, 0, 0);
+	const uint32_t c = crc ^ w;
+	return c_crc32c.t[3][c & 0xffu] ^ c_crc32c.t[2][(c >> 8) & 0xffu] ^
+	       c_crc32c.t[1][(c >> 16) & 0xffu] ^ c_crc32c.t[0][c >> 24];
+}
+
+// Value of lane `src` (every lane of the wave must be active: callers keep
+// the control flow uniform around it).
+__device__ __forceinline__ uint32_t lane_get(uint32_t v, uint32_t src)
+{
+	return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v);
+}
+
+// Inclusive prefix sum over the 64 lanes of the wave (all lanes active).
+__device__ __forceinline__ uint32_t wave_scan_add(uint32_t v, uint32_t lane)
+{
 #pragma unroll
-		for (uint32_t j = 0; j < 4; ++j) {
-			const uint32_t q = p + 4u * j;
-			const uint32_t lo = from > q ? min(from - q, 4u) : 0u;
-			const uint32_t hi = to > q ? min(to - q, 4u) : 0u;
-			const uint32_t mhi = hi >= 4u ? ~0u : ((1u << (8u * hi)) - 1u);
-			const uint32_t mlo = lo >= 4u ? ~0u : ((1u << (8u * lo)) - 1u);
-			s += v[j] & mhi & ~mlo;
-		}
+	for (uint32_t d = 1; d < WAVE; d <<= 1) {
+		const uint32_t t = lane_get(v, lane >= d ? lane - d : lane);
+		v += lane >= d ? t : 0u;
 	}
-	return s;
+	return v;
 }
 
-// _odp_packet_l4_chksum (odp_packet.c:2065-2138) for a parse that returned
-// 0, with the partial sums parse_ipv4 / parse_ipv6 / parse_tcp / parse_udp /
-// parse_sctp prepare (odp_parse.c:146-148, 212-214, 267-275, 298-313,
-// 341-351): UDP / TCP one's-complement sum over the pseudo header and
-// [l4, frame_len), SCTP CRC-32C over [l4, frame_len) with the checksum field
-// taken as zero.  Fragments are skipped.  A failure sets l4_chksum_err and
-// the protocol's error bit, and drops the packet under drop_<proto>_err.
-__device__ __forceinline__ void l4_chksum(const Pkt &k, Parsed &p, uint32_t opt,
-					  __amdgpu_buffer_rsrc_t rs, uint32_t boff)
+// 16-B pieces of the cooperative one's-complement sum in flight per lane
+#ifndef CK_UNROLL
+#define CK_UNROLL 4
+#endif
+
+// Wave-cooperative one's-complement sums of the UDP / TCP payloads of a
+// tile (all 64 lanes active).  Lane f asks for the sum of frame bytes
+// [from, to) of its frame: `cnt` 16-B pieces starting at batch offset `base`
+// (the frame-relative 16-B boundary at or below `from`), with
+// prm = (from - boundary) | (to - boundary) << 4.  The pieces of all lanes
+// are numbered in lane order (a wave prefix sum of cnt) and dealt out 64 per
+// round: lane j of a round loads piece g = round base + j, which belongs to
+// the last lane whose first piece number is <= g (binary search over the
+// lanes' first numbers with ds_bpermute).  Consecutive pieces are
+// consecutive bytes of one frame and the frames of a tile are consecutive in
+// the batch, so one load instruction reads ~1 KB of contiguous bytes instead
+// of 16 B from each of 64 frames, and every lane is busy whatever the frame
+// lengths are (the per-lane loop ran every lane for the longest frame of the
+// tile).  Each piece is folded to a 19-bit value congruent to its sum of
+// 16-bit words modulo 0xffff (2^16 == 1), a prefix sum over the round gives
+// each owner its pieces' total as the difference of two prefix values.
+// Returns the lane's own sum (congruent mod 0xffff, < 2^32).
+__device__ __forceinline__ uint32_t ck_sum_wave(__amdgpu_buffer_rsrc_t rs, uint32_t base,
+						uint32_t prm, uint32_t cnt, uint32_t lane)
 {
-	if (p.ret != 0 || (p.flags & F_IPFRAG))
-		return;
-	const uint32_t f = p.flags, len = k.len, l3 = p.l3, l4 = p.l4;
-	const uint32_t kind = ((opt & OPT_UDP_CK) && (f & F_UDP) && !p.udp_zero) ? 1u
-		: (((opt & OPT_TCP_CK) && (f & F_TCP)) ? 2u
-		: (((opt & OPT_SCTP_CK) && (f & F_SCTP)) ? 3u : 0u));
-	if (kind == 0u)
-		return;
-	bool bad;
-	if (kind < 3u) {
-		uint64_t s = 0;
-		if (f & F_IPV4) {
-			s = (uint64_t)r32(k, l3 + 12u) + r32(k, l3 + 16u);
-		} else {
-			for (uint32_t i = 0; i < 8u; ++i)
-				s += r32(k, l3 + 8u + 4u * i);
+	const uint32_t incl = wave_scan_add(cnt, lane);
+	const uint32_t first = incl - cnt;   // number of this lane's first piece
+	const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, WAVE - 1);
+	uint32_t acc = 0;
+	for (uint32_t B = 0; B < total; B += CK_UNROLL * WAVE) {
+		u32x4 v[CK_UNROLL];
+		uint32_t pr[CK_UNROLL], q16[CK_UNROLL];
+#pragma unroll
+		for (uint32_t u = 0; u < CK_UNROLL; ++u) {
+			const uint32_t g = B + u * WAVE + lane;
+			uint32_t lo = 0;
+#pragma unroll
+			for (uint32_t s = WAVE / 2; s >= 1; s >>= 1) {
+				const uint32_t c = lo + s;
+				lo = lane_get(first, c) <= g ? c : lo;
+			}
+			const uint32_t q = g - lane_get(first, lo);
+			pr[u] = lane_get(prm, lo);
+			q16[u] = 16u * q;
+			const uint32_t ob = lane_get(base, lo);
+			v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, g < total ? ob + q16[u] : OOB_OFF,
+								     0, 0);
 		}
-		if (kind == 1u)   // udp->length as stored, IPPROTO_UDP << 8
-			s += r16(k, l4 + 4u) + (17u << 8);
-		else              // odp_cpu_to_be_16(frame_len - l4), IPPROTO_TCP << 8
-			s += (((len - l4) & 0xffu) << 8) + (((len - l4) >> 8) & 0xffu) + (6u << 8);
-		s += ck_sum_frame(rs, boff, l4, len);
-		bad = ck_finalize(s) != 0xffffu;   // ~sum != 0
-	} else {
-		uint32_t crc = 0xffffffffu;
-		for (uint32_t i = 0; i < 8u; ++i)
-			crc = crc32c_u8(crc, rb(k, l4 + i));
-		for (uint32_t i = 0; i < 4u; ++i)
-			crc = crc32c_u8(crc, 0u);
-		for (uint32_t o = l4 + 12u; o < len; ++o)
-			crc = crc32c_u8(crc, rb(k, o));
-		bad = ~crc != r32(k, l4 + 8u);
+#pragma unroll
+		for (uint32_t u = 0; u < CK_UNROLL; ++u) {
+			const uint32_t from = pr[u] & 15u, to = pr[u] >> 4;
+			uint64_t s = 0;
+#pragma unroll
+			for (uint32_t j = 0; j < 4; ++j) {
+				const uint32_t qq = q16[u] + 4u * j;
+				const uint32_t lo = from > qq ? min(from - qq, 4u) : 0u;
+				const uint32_t hi = to > qq ? min(to - qq, 4u) : 0u;
+				const uint32_t mhi = hi >= 4u ? ~0u : ((1u << (8u * hi)) - 1u);
+				const uint32_t mlo = lo >= 4u ? ~0u : ((1u << (8u * lo)) - 1u);
+				s += v[u][j] & mhi & ~mlo;
+			}
+			// < 2^18 + 2^16; pieces past the last one (g >= total) read 0
+			const uint32_t r = (uint32_t)(s & 0xffffu) + (uint32_t)(s >> 16);
+			const uint32_t P = wave_scan_add(r, lane);
+			// this lane's pieces in the round: lanes [a, e) of it
+			const uint32_t rb0 = B + u * WAVE;
+			const uint32_t a = first > rb0 ? first - rb0 : 0u;
+			const uint32_t e = min(incl > rb0 ? incl - rb0 : 0u, (uint32_t)WAVE);
+			const uint32_t pe = lane_get(P, e > 0u ? e - 1u : 0u);
+			const uint32_t pa = lane_get(P, a > 0u ? a - 1u : 0u);
+			acc += (e > a) ? pe - (a > 0u ? pa : 0u) : 0u;
+		}
 	}
-	p.flags |= F_L4CK_DONE;
-	if (bad) {
-		p.err |= E_L4CK | (kind == 1u ? E_UDP : (kind == 2u ? E_TCP : E_SCTP));
-		const uint32_t d = kind == 1u ? OPT_DROP_UDP : (kind == 2u ? OPT_DROP_TCP : OPT_DROP_SCTP);
-		p.ret = (opt & d) ? -1 : 1;
+	return acc;
+}
+
+// CRC-32C part of the SCTP check (odp_packet.c:2112-2131 via
+// _odp_packet_sctp_chksum): over [l4, frame_len) with the 4-byte checksum
+// field at l4 + 8 taken as zero, init ~0, four bytes per step from aligned
+// dword loads of the frame (funnel-shifted when l4 is 2 mod 4), the last
+// 0-3 bytes one at a time.  Returns the finished (inverted) CRC.
+__device__ __forceinline__ uint32_t sctp_crc(const Pkt &k, __amdgpu_buffer_rsrc_t rs, uint32_t boff,
+					     uint32_t l4)
+{
+	const uint32_t len = k.len, sh = l4 & 3u, n4 = (len - l4) >> 2;
+	uint32_t j = l4 >> 2;
+	uint32_t prev = __builtin_amdgcn_raw_buffer_load_b32(rs, boff + 4u * j, 0, 0);
+	uint32_t crc = 0xffffffffu;
+	for (uint32_t i = 0; i < n4; ++i) {
+		++j;
+		// dword 4j reaches at most 4 - sh bytes past the word: never past the
+		// frame's 16-B rounding (the batch contract)
+		const uint32_t next = __builtin_amdgcn_raw_buffer_load_b32(rs, boff + 4u * j, 0, 0);
+		const uint32_t w = __builtin_amdgcn_alignbyte(next, prev, sh);
+		crc = crc32c_u32(crc, i == 2u ? 0u : w);
+		prev = next;
+	}
+	for (uint32_t o = l4 + 4u * n4; o < len; ++o)
+		crc = crc32c_u8(crc, rb(k, o));
+	return ~crc;
+}
+
+// _odp_packet_l4_chksum (odp_packet.c:2065-2138) for the lanes whose parse
+// returned 0, with the partial sums parse_ipv4 / parse_ipv6 / parse_tcp /
+// parse_udp / parse_sctp prepare (odp_parse.c:146-148, 212-214, 267-275,
+// 298-313, 341-351): UDP / TCP one's-complement sum over the pseudo header
+// and [l4, frame_len) (ck_sum_wave, the whole wave cooperating), SCTP
+// CRC-32C over [l4, frame_len) with the checksum field taken as zero.
+// Fragments are skipped.  A failure sets l4_chksum_err and the protocol's
+// error bit, and drops the packet under drop_<proto>_err.  Called with every
+// lane of the wave active.
+__device__ __forceinline__ void l4_chksum(const Pkt &k, Parsed &p, uint32_t opt,
+					  __amdgpu_buffer_rsrc_t rs, uint32_t boff, uint32_t lane,
+					  bool valid)
+{
+	const uint32_t f = p.flags, len = k.len, l3 = p.l3, l4 = p.l4;
+	const bool go = valid && p.ret == 0 && !(f & F_IPFRAG);
+	const uint32_t kind = !go ? 0u
+		: (((opt & OPT_UDP_CK) && (f & F_UDP) && !p.udp_zero) ? 1u
+		: (((opt & OPT_TCP_CK) && (f & F_TCP)) ? 2u
+		: (((opt & OPT_SCTP_CK) && (f & F_SCTP)) ? 3u : 0u)));
+	const bool sum = kind == 1u || kind == 2u;
+	uint64_t s = 0;
+	uint32_t cnt = 0, base = 0, prm = 0;
+	if (__ballot(sum) != 0ull) {
+		if (sum) {
+			if (f & F_IPV4) {
+				s = (uint64_t)r32(k, l3 + 12u) + r32(k, l3 + 16u);
+			} else {
+				for (uint32_t i = 0; i < 8u; ++i)
+					s += r32(k, l3 + 8u + 4u * i);
+			}
+			if (kind == 1u)   // udp->length as stored, IPPROTO_UDP << 8
+				s += r16(k, l4 + 4u) + (17u << 8);
+			else              // odp_cpu_to_be_16(frame_len - l4), IPPROTO_TCP << 8
+				s += (((len - l4) & 0xffu) << 8) + (((len - l4) >> 8) & 0xffu) + (6u << 8);
+			// the parse guarantees l4 + 8 <= len (UDP) / l4 + 20 <= len (TCP)
+			const uint32_t p0 = l4 & ~15u;
+			cnt = (len - p0 + 15u) >> 4;
+			base = boff + p0;
+			prm = (l4 - p0) | ((len - p0) << 4);
+		}
+		s += ck_sum_wave(rs, base, prm, cnt, lane);
+	}
+	bool bad = sum && ck_finalize(s) != 0xffffu;   // ~sum != 0
+	if (__ballot(kind == 3u) != 0ull) {
+		if (kind == 3u)
+			bad = sctp_crc(k, rs, boff, l4) != r32(k, l4 + 8u);
+	}
+	if (kind != 0u) {
+		p.flags |= F_L4CK_DONE;
+		if (bad) {
+			p.err |= E_L4CK | (kind == 1u ? E_UDP : (kind == 2u ? E_TCP : E_SCTP));
+			const uint32_t d = kind == 1u ? OPT_DROP_UDP : (kind == 2u ? OPT_DROP_TCP : OPT_DROP_SCTP);
+			p.ret = (opt & d) ? -1 : 1;
+		}
 	}
 }
 
@@ -1362,10 +1481,6 @@ __device__ __forceinline__ bool stats_bit(const KArgs &a, uint32_t c)
 	return c < MAX_STATS_COS && ((a.stats_mask[c >> 5] >> (c & 31u)) & 1u);
 }
 
-// Buffer offset no frame byte reaches: num_records of the packet resource, so
-// a load at or past it returns zeros (batches are < 4 GiB: u32 offsets).
-#define OOB_OFF 0xFFFFFE00u
-
 static_assert(NPIECE == 8 || NPIECE == 6, "WIN must be 96 or 128");
 #define NB (NPIECE - 4)         // upper pieces (phase B)
 
@@ -1504,7 +1619,11 @@ constexpr int waves_per_eu(int nw)
 // without rules), and no pktin option is set: no descent loop, no linear
 // scan, no checksum path in the code (fewer registers, straight-line
 // engine).  The host picks it only for such programs (mi_cls_classify).
-template <bool LT, bool DIV, int NW, int FM = -1>
+// CK: pktin-option kernel (mi_cls_kc.hip), launched whenever a pktin
+// checksum / drop option is set; the other kernels require opt == 0 and carry
+// no option code (the checksum path's registers would otherwise be
+// allocated, and spilled, in every kernel).
+template <bool LT, bool DIV, int NW, int FM = -1, bool CK = false>
 __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KArgs a)
 {
 	__shared__ uint32_t s_win[NW * RS * WROWS];
@@ -1663,19 +1782,32 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 
 		STAMP(1);   // next tile's loads issued
 		Parsed p;
-		if (FM >= 0 || a.opt == 0u) {
+		if constexpr (!CK) {
 			bool slow;
 			p = parse_fast(k, s_l4, slow);
 			if (__ballot(slow) != 0ull) {
 				if (slow)
 					p = parse_packet(k, 0u);
 			}
-		} else if constexpr (FM < 0) {
-			// pktin checksum / drop options: the general parser for every
-			// lane, then the L4 checksums (whole frames from HBM)
-			p = parse_packet(k, a.opt);
+		} else {
+			// pktin options.  Checksum options: the general parser for every
+			// lane, then the L4 checksums (whole frames from HBM, the wave
+			// cooperating).  Drop options alone act only on lanes whose
+			// parse reports an error, so the fast parse stands for every
+			// other lane and only those are re-parsed with the options.
+			if (a.opt & (OPT_IPV4_CK | OPT_L4_CK)) {
+				p = parse_packet(k, a.opt);
+			} else {
+				bool slow;
+				p = parse_fast(k, s_l4, slow);
+				slow = slow || p.err != 0u;
+				if (__ballot(slow) != 0ull) {
+					if (slow)
+						p = parse_packet(k, a.opt);
+				}
+			}
 			if (a.opt & OPT_L4_CK)
-				l4_chksum(k, p, a.opt, rs, my_off);
+				l4_chksum(k, p, a.opt, rs, my_off, lane, valid);
 		}
 		const Fields x = fields_of(k, p);
 		{
@@ -1875,3 +2007,6 @@ int mi_cls_launch_k16(bool lt, bool div, unsigned grid, size_t dyn, hipStream_t 
 // flat-program kernels (FM = engine of the default CoS block; NW 4, 12, 16;
 // hot region in LDS): mi_cls_kf.hip
 int mi_cls_launch_flat(int nw, int fm, unsigned grid, size_t dyn, hipStream_t st, const KArgs &a);
+// pktin-option kernels (CK; NW 4 or 16): mi_cls_kc.hip
+int mi_cls_launch_ck(int nw, bool lt, bool div, unsigned grid, size_t dyn, hipStream_t st,
+		     const KArgs &a);

@@ -224,7 +224,7 @@ def _put_be32(h, col, v):
 
 def build_batch(lens, *, ipver, l4proto, sip4=None, dip4=None, sip6=None, dip6=None,
                 sport, dport, ntags=None, vid0=None, vid1=None, tos=None, seed=0) -> Batch:
-    """Vectorised Eth[/VLAN/QinQ]/(IPv4|IPv6)/(UDP|TCP) batch.
+    """Vectorised Eth[/VLAN/QinQ]/(IPv4|IPv6)/(UDP|TCP|SCTP) batch.
 
     All arguments are per-packet arrays.  ntags: 0 untagged, 1 802.1Q (vid0),
     2 QinQ (0x88A8 vid0 outer, 0x8100 vid1 inner).  IP/UDP length fields are
@@ -236,7 +236,8 @@ def build_batch(lens, *, ipver, l4proto, sip4=None, dip4=None, sip6=None, dip6=N
         ntags = np.zeros(n, np.int64)
     # never emit a frame shorter than its own headers
     hdr_len = 14 + 4 * np.asarray(ntags) + np.where(np.asarray(ipver) == 6, 40, 20) + \
-        np.where(np.asarray(l4proto) == IPPROTO_TCP, 20, 8)
+        np.where(np.asarray(l4proto) == IPPROTO_TCP, 20,
+                 np.where(np.asarray(l4proto) == IPPROTO_SCTP, 12, 8))
     lens = np.maximum(lens.astype(np.int64), hdr_len)
     off, total = _layout(lens)
     rng = np.random.default_rng(seed ^ 0x5EED)
@@ -246,7 +247,7 @@ def build_batch(lens, *, ipver, l4proto, sip4=None, dip4=None, sip6=None, dip6=N
     H = 18 + 4 * 2 + 40 + 20 + 2  # max header span we write
     for nt in (0, 1, 2):
         for v in (4, 6):
-            for p in (IPPROTO_UDP, IPPROTO_TCP):
+            for p in (IPPROTO_UDP, IPPROTO_TCP, IPPROTO_SCTP):
                 sel = np.nonzero((ntags == nt) & (ipver == v) & (l4proto == p))[0]
                 if sel.size == 0:
                     continue
@@ -299,6 +300,9 @@ def build_batch(lens, *, ipver, l4proto, sip4=None, dip4=None, sip6=None, dip6=N
                 if p == IPPROTO_UDP:
                     _put_be16(h, l4 + 4, l4_len)
                     hl = l4 + 8
+                elif p == IPPROTO_SCTP:
+                    _put_be32(h, l4 + 4, 0x5C7F0001)   # verification tag; CRC 0
+                    hl = l4 + 12
                 else:
                     _put_be32(h, l4 + 4, 1)
                     h[:, l4 + 12] = 0x50
@@ -319,10 +323,34 @@ def build_batch(lens, *, ipver, l4proto, sip4=None, dip4=None, sip6=None, dip6=N
     return Batch(buf, off.astype(np.uint32), lens.astype(np.uint16))
 
 
+def _crc32c_tables():
+    t = np.zeros(256, np.uint32)
+    for i in range(256):
+        c = i
+        for _ in range(8):
+            c = (c >> 1) ^ 0x82F63B78 if c & 1 else c >> 1
+        t[i] = c
+    return t
+
+
+_CRC32C = _crc32c_tables()
+
+
+def sctp_crc32c(frames: np.ndarray) -> np.ndarray:
+    """CRC-32C (init ~0, final inversion) of each row of a uint8 matrix,
+    vectorised over rows: the SCTP checksum of RFC 4960 appendix B."""
+    crc = np.full(frames.shape[0], 0xFFFFFFFF, np.uint32)
+    for j in range(frames.shape[1]):
+        crc = _CRC32C[(crc ^ frames[:, j]) & 0xFF] ^ (crc >> np.uint32(8))
+    return ~crc
+
+
 def set_checksums(b: Batch, l3: int = 14) -> Batch:
-    """Write valid IPv4 header and UDP / TCP checksums (RFC 1071 sums, RFC 768
-    / 793 / 8200 pseudo headers) into an untagged build_batch() batch (IPv4
-    IHL 5 or IPv6 without extension headers), in place, vectorised."""
+    """Write a valid IPv4 header checksum and valid L4 checksums into an
+    untagged build_batch() batch (IPv4 IHL 5 or IPv6 without extension
+    headers), in place, vectorised: RFC 1071 sums with the RFC 768 / 793 /
+    8200 pseudo headers for UDP and TCP, CRC-32C (RFC 4960) for SCTP.  Other
+    L4 protocols are left alone."""
     buf = b.buf
     off = b.off.astype(np.int64)
     ln = b.len.astype(np.int64)
@@ -338,6 +366,7 @@ def set_checksums(b: Batch, l3: int = 14) -> Batch:
 
     et = (buf[off + 12].astype(np.int64) << 8) | buf[off + 13]
     v4 = et == ETH_IPV4
+    v6 = et == ETH_IPV6
     o4 = off[v4] + l3
     buf[o4 + 10] = 0
     buf[o4 + 11] = 0
@@ -345,24 +374,50 @@ def set_checksums(b: Batch, l3: int = 14) -> Batch:
     buf[o4 + 10] = (c >> 8).astype(np.uint8)
     buf[o4 + 11] = (c & 0xFF).astype(np.uint8)
 
-    proto = np.where(v4, buf[off + l3 + 9], buf[off + l3 + 6]).astype(np.int64)
+    proto = np.where(v4, buf[off + l3 + 9], np.where(v6, buf[off + l3 + 6], 0)).astype(np.int64)
     l4 = off + np.where(v4, l3 + 20, l3 + 40)
-    l4_len = off + ln - l4
-    cko = l4 + np.where(proto == IPPROTO_UDP, 6, 16)
-    buf[cko] = 0
-    buf[cko + 1] = 0
-    # source + destination address words
-    pseudo = words(off + l3 + 12, 4) if v4.all() else np.where(
-        v4, words(off + l3 + 12, 4), words(off + l3 + 8, 16))
-    pseudo = pseudo + proto + l4_len
-    w = buf[: buf.size // 2 * 2].reshape(-1, 2).astype(np.int64)
-    cs = np.concatenate([[0], np.cumsum((w[:, 0] << 8) | w[:, 1])])
     end = off + ln
-    s = cs[end // 2] - cs[l4 // 2] + np.where(end % 2 == 1, buf[end - 1].astype(np.int64) << 8, 0)
-    c = ~fold(pseudo + s) & 0xFFFF
-    c = np.where((proto == IPPROTO_UDP) & (c == 0), 0xFFFF, c)
-    buf[cko] = (c >> 8).astype(np.uint8)
-    buf[cko + 1] = (c & 0xFF).astype(np.uint8)
+
+    # UDP / TCP: 16-bit one's-complement sum over pseudo header + segment
+    sel = np.nonzero((v4 | v6) & ((proto == IPPROTO_UDP) | (proto == IPPROTO_TCP)))[0]
+    if sel.size:
+        l4s, ends, pr, v4s = l4[sel], end[sel], proto[sel], v4[sel]
+        cko = l4s + np.where(pr == IPPROTO_UDP, 6, 16)
+        buf[cko] = 0
+        buf[cko + 1] = 0
+        o = off[sel]
+        pseudo = np.where(v4s, words(o + l3 + 12, 4), words(o + l3 + 8, 16)) if not v4s.all() \
+            else words(o + l3 + 12, 4)
+        pseudo = pseudo + pr + (ends - l4s)
+        # prefix sums of big-endian 16-bit words at even and at odd buffer
+        # offsets (frames may start at either parity)
+        s = np.zeros(sel.size, np.int64)
+        for par in (0, 1):
+            m = (l4s % 2) == par
+            if not m.any():
+                continue
+            nw = (buf.size - par) // 2
+            wp = (buf[par: par + 2 * nw: 2].astype(np.int64) << 8) | buf[par + 1: par + 2 * nw: 2]
+            cs = np.concatenate([[0], np.cumsum(wp)])
+            del wp
+            a, e = (l4s[m] - par) // 2, (ends[m] - par) // 2
+            odd = (ends[m] - l4s[m]) % 2 == 1
+            s[m] = cs[e] - cs[a] + np.where(odd, buf[ends[m] - 1].astype(np.int64) << 8, 0)
+        c = ~fold(pseudo + s) & 0xFFFF
+        c = np.where((pr == IPPROTO_UDP) & (c == 0), 0xFFFF, c)
+        buf[cko] = (c >> 8).astype(np.uint8)
+        buf[cko + 1] = (c & 0xFF).astype(np.uint8)
+
+    # SCTP: CRC-32C over the common header (checksum field zero) and chunks,
+    # stored little-endian (the reference compares the raw 32-bit field)
+    sel = np.nonzero((v4 | v6) & (proto == IPPROTO_SCTP))[0]
+    for seg_len in np.unique(end[sel] - l4[sel]):
+        g = sel[(end[sel] - l4[sel]) == seg_len]
+        idx = l4[g][:, None] + np.arange(int(seg_len))[None, :]
+        buf[l4[g][:, None] + 8 + np.arange(4)[None, :]] = 0
+        crc = sctp_crc32c(buf[idx])
+        for i in range(4):
+            buf[l4[g] + 8 + i] = ((crc >> np.uint32(8 * i)) & np.uint32(0xFF)).astype(np.uint8)
     return b
 
 

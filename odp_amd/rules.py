@@ -190,14 +190,18 @@ def _target_fields(rules, n, rng, hit_frac, sizes):
     return sip, dip, proto, dport
 
 
-def config3(n=1_000_000, num_rules=256, size="imix", rank=0):
+def config3(n=1_000_000, num_rules=256, size="imix", rank=0, sctp_frac=0.0):
     """BASELINE config 3: n IMIX (60/566/1514 B, 7:4:1, shuffled) IPv4 packets,
     80 % UDP / 20 % TCP; num_rules 2-3-term PMRs over {SIP/DIP prefix,
-    IPPROTO, UDP/TCP dport} on the default CoS; ~30 % match nothing."""
+    IPPROTO, UDP/TCP dport} on the default CoS; ~30 % match nothing.
+    sctp_frac > 0 turns that fraction of the packets into SCTP (the
+    checksum-validation bench's SCTP line)."""
     rng = np.random.default_rng(pg.seed_for(3) + 7919 * rank)
     rules = _l34_rules(num_rules, 32, rng)
     lens = pg.imix_lens(rng, n) if size == "imix" else np.full(n, int(size))
     sip, dip, proto, dport = _target_fields(rules, n, rng, 0.7, lens)
+    if sctp_frac > 0:
+        proto = np.where(rng.random(n) < sctp_frac, pg.IPPROTO_SCTP, proto)
     b = pg.build_batch(lens, ipver=np.full(n, 4), l4proto=proto, sip4=sip, dip4=dip,
                        sport=rng.integers(1024, 65535, n), dport=dport, seed=3 + rank)
     prog = [cos("default", queue=1)] + [cos(f"c{i}", queue=100 + i) for i in range(32)]

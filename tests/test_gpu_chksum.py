@@ -84,3 +84,40 @@ def test_checksum_imix_configs(built, gpu, cfg):
     b, prog = R.CONFIGS[cfg](20_000)
     both(prog, b, CK.ALL_CK, f"config {cfg}")
     both(prog, b, CK.UDP_CK | CK.TCP_CK | CK.SCTP_CK | CK.ALL_DROP, f"config {cfg} l4")
+
+
+@pytest.mark.parametrize("ipver", [4, 6])
+def test_checksum_valid_mixed_lengths(built, gpu, ipver):
+    """Valid UDP / TCP / SCTP checksums (pktgen.set_checksums) over IMIX,
+    odd and jumbo (up to 9000 B: hundreds of 16-B pieces spread over many
+    rounds of the wave-cooperative sum) lengths, then a payload byte flipped
+    in every 7th frame: GPU == oracle, and the verdicts are the constructed
+    ones (only the flipped frames fail)."""
+    rng = np.random.default_rng(40 + ipver)
+    n = 6000
+    lens = pg.imix_lens(rng, n)
+    pick = rng.random(n)
+    lens = np.where(pick < 0.05, rng.integers(1515, 9001, n), lens)
+    lens = np.where((pick > 0.5) & (pick < 0.6), rng.integers(61, 1514, n), lens)
+    proto = rng.choice([pg.IPPROTO_UDP, pg.IPPROTO_TCP, pg.IPPROTO_SCTP], n)
+    kw = dict(sip4=rng.integers(0, 2**32, n).astype(np.uint64),
+              dip4=rng.integers(0, 2**32, n).astype(np.uint64)) if ipver == 4 else dict(
+        sip6=rng.integers(0, 256, (n, 16), dtype=np.uint8),
+        dip6=rng.integers(0, 256, (n, 16), dtype=np.uint8))
+    b = pg.build_batch(lens, ipver=np.full(n, ipver), l4proto=proto,
+                       sport=rng.integers(1, 65535, n), dport=rng.integers(1, 65535, n),
+                       seed=11, **kw)
+    pg.set_checksums(b)
+    l4 = 14 + (20 if ipver == 4 else 40)
+    bad = np.zeros(n, bool)
+    for i in range(0, n, 7):
+        o, ln = int(b.off[i]), int(b.len[i])
+        if ln > l4 + 20:   # a payload byte (never a checksum field)
+            b.buf[o + int(rng.integers(l4 + 20, ln))] ^= 0x5A
+            bad[i] = True
+    prog = [R.cos("d", queue=1), ("default", 0)]
+    got = both(prog, b, CK.ALL_CK, f"valid ipv{ipver}")
+    l4_err = (got["err"] & CK.E_L4CK) != 0
+    assert ((got["in_flags"] >> 31) & 1).all()
+    assert np.array_equal(l4_err, bad)
+    both(prog, b, CK.ALL_CK | CK.ALL_DROP, f"valid ipv{ipver} drop")

@@ -13,6 +13,7 @@ import numpy as np
 import pytest
 
 from odp_amd import pktgen as pg
+from odp_amd import rules as R
 from oracle import oracle as O
 from tests import chksum_frames as CK
 from tests import zoo
@@ -123,3 +124,36 @@ def test_fragments_skip_l4_checksum():
     bad = CK.corrupt(rng, bytes(b), l4 + 8, len(b)) if len(b) > l4 + 8 else bytes(b)
     r, f, e, _, _, _ = O.parse(bad, CK.ALL_CK)
     assert r == 0 and (f >> 30) & 1 and not (f >> 31) & 1 and e == 0
+
+
+@pytest.mark.parametrize("ipver", [4, 6])
+def test_pktgen_set_checksums_all_ok(ipver):
+    """pktgen.set_checksums (the checksum bench's input) writes valid IPv4,
+    UDP, TCP and SCTP checksums: with every pktin checksum and drop option
+    set, the oracle validates every packet and reports no error; the SCTP
+    CRC also equals the independent RFC 4960 construction here."""
+    rng = np.random.default_rng(5 + ipver)
+    n = 600
+    lens = pg.imix_lens(rng, n)
+    lens[:4] = [61, 567, 1513, 99]              # odd lengths
+    proto = rng.choice([pg.IPPROTO_UDP, pg.IPPROTO_TCP, pg.IPPROTO_SCTP], n)
+    kw = dict(sip4=rng.integers(0, 2**32, n).astype(np.uint64),
+              dip4=rng.integers(0, 2**32, n).astype(np.uint64)) if ipver == 4 else dict(
+        sip6=rng.integers(0, 256, (n, 16), dtype=np.uint8),
+        dip6=rng.integers(0, 256, (n, 16), dtype=np.uint8))
+    b = pg.build_batch(lens, ipver=np.full(n, ipver), l4proto=proto,
+                       sport=rng.integers(1, 65535, n), dport=rng.integers(1, 65535, n),
+                       seed=9, **kw)
+    pg.set_checksums(b)
+    o = O.Oracle(pktin_opt=CK.ALL_CK | CK.ALL_DROP)
+    o.apply([R.cos("d", queue=1), ("default", 0)])
+    r = o.classify(b)
+    assert (r["err"] == 0).all()
+    assert ((r["in_flags"] >> 31) & 1).all()                  # every L4 checksum validated
+    assert ((r["in_flags"] >> 30) & 1).all() == (ipver == 4)  # IPv4 header checksums
+    for i in np.nonzero(proto == pg.IPPROTO_SCTP)[0][:20]:
+        f = bytearray(b.frame(i))
+        l4 = 14 + (20 if ipver == 4 else 40)
+        want = int.from_bytes(f[l4 + 8: l4 + 12], "little")
+        f[l4 + 8: l4 + 12] = b"\0\0\0\0"
+        assert (~CK.crc32c(bytes(f[l4:]))) & 0xFFFFFFFF == want
