@@ -482,10 +482,16 @@ static bool build_bv(const mi_cos_t *cs, const mi_rule_t *rs, const mi_term_t *t
 	blk[0] = mode;
 	blk[1] = ncls;
 	blk[3] = wc_first;
+	auto res_word = [&](uint32_t r) {
+		return (rs[r].dst_cos & 0xffu) | (cs[rs[r].dst_cos].num_rules == 0 ? 0x100u : 0u) |
+		       ((uint32_t)rs[r].mark << 16);
+	};
+	// direct blocks keep each rule's result word in the table slot itself
+	// (no results array, no second lookup); the others index this array
 	blk[2] = base + (uint32_t)blk.size();
-	for (uint32_t r = 0; r < nrules; ++r)
-		blk.push_back((rs[r].dst_cos & 0xffu) | (cs[rs[r].dst_cos].num_rules == 0 ? 0x100u : 0u) |
-			      ((uint32_t)rs[r].mark << 16));
+	if (mode != 0u)
+		for (uint32_t r = 0; r < nrules; ++r)
+			blk.push_back(res_word(r));
 	std::vector<std::vector<std::vector<uint32_t>>> lists(ncls);   // [class][key id] -> rules
 	// wide rows: 8 words each (zero past the rule count), deduplicated.  Every
 	// row id is assigned before the layout is emitted (mode 3 below): rows
@@ -626,7 +632,8 @@ static bool build_bv(const mi_cos_t *cs, const mi_rule_t *rs, const mi_term_t *t
 		const uint32_t SW = ck.nkey + 1u;   // slot: key words, value
 		blk[cbase + 0] = ck.kind;
 		blk[cbase + 1] = ck.nkey;
-		const uint32_t miss = mode == 0u ? first_live(c, nullptr)
+		const uint32_t fl0 = mode == 0u ? first_live(c, nullptr) : 0u;
+		const uint32_t miss = mode == 0u ? (fl0 == BV_NONE ? 0u : res_word(fl0) | BV_RES_VALID)
 			: (mode == 2u ? row_of(c, nullptr) : (mode == 3u ? base + rows_at + 4u * miss_id[c] : 0u));
 		blk[cbase + 2] = miss;
 		blk[cbase + 3] = ck.offset;
@@ -678,7 +685,7 @@ static bool build_bv(const mi_cos_t *cs, const mi_rule_t *rs, const mi_term_t *t
 			uint32_t val;
 			if (mode == 0u) {
 				const uint32_t f = first_live(c, &keys[i]);
-				val = f == BV_NONE ? BV_EMPTY : f + 1u;
+				val = f == BV_NONE ? BV_EMPTY : res_word(f) | BV_RES_VALID;
 			} else if (mode == 2u) {
 				val = row_of(c, &keys[i]);   // non-zero: the key's own rules
 			} else if (mode == 3u) {
@@ -1002,8 +1009,11 @@ extern "C" int mi_cls_classify(mi_cls_ctx_t *c, const uint8_t *pkts, const uint3
 	const int wpb_env = c->wpb;
 	const size_t LDS_CU = 160u * 1024u;
 	const size_t hot_bytes = (((size_t)c->hot_words + 3u) & ~(size_t)3u) * sizeof(uint32_t);
-	auto st_of = [](int w) {
-		return sizeof(uint32_t) * ((size_t)w * RS * WROWS + MAX_STATS_COS + 256);
+	// static LDS of a block: windows, stats histogram, L4 table (+ the
+	// CRC-32C tables of the pktin-option kernels)
+	const size_t st_ck = c->opt != 0 ? 1024 : 0;
+	auto st_of = [st_ck](int w) {
+		return sizeof(uint32_t) * ((size_t)w * RS * WROWS + MAX_STATS_COS + 256 + st_ck);
 	};
 	const bool small = (long)hot_bytes <= (long)hot_max;
 	const bool full4 = small && 4 * (st_of(4) + hot_bytes) <= LDS_CU;

@@ -431,17 +431,19 @@ struct Crc32cTab {
 };
 static __constant__ Crc32cTab c_crc32c;
 
-__device__ __forceinline__ uint32_t crc32c_u8(uint32_t crc, uint32_t b)
+// Table lookups go to the kernel's LDS copy of c_crc32c (`tab`, 4 x 256
+// words): a lane walks its own frame, so the lookups are divergent.
+__device__ __forceinline__ uint32_t crc32c_u8(const uint32_t *tab, uint32_t crc, uint32_t b)
 {
-	return c_crc32c.t[0][(crc ^ b) & 0xffu] ^ (crc >> 8);
+	return tab[(crc ^ b) & 0xffu] ^ (crc >> 8);
 }
 
 // four bytes, little-endian word w (byte 0 first on the wire)
-__device__ __forceinline__ uint32_t crc32c_u32(uint32_t crc, uint32_t w)
+__device__ __forceinline__ uint32_t crc32c_u32(const uint32_t *tab, uint32_t crc, uint32_t w)
 {
 	const uint32_t c = crc ^ w;
-	return c_crc32c.t[3][c & 0xffu] ^ c_crc32c.t[2][(c >> 8) & 0xffu] ^
-	       c_crc32c.t[1][(c >> 16) & 0xffu] ^ c_crc32c.t[0][c >> 24];
+	return tab[768u + (c & 0xffu)] ^ tab[512u + ((c >> 8) & 0xffu)] ^
+	       tab[256u + ((c >> 16) & 0xffu)] ^ tab[c >> 24];
 }
 
 // Value of lane `src` (every lane of the wave must be active: callers keep
@@ -451,39 +453,42 @@ __device__ __forceinline__ uint32_t lane_get(uint32_t v, uint32_t src)
 	return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v);
 }
 
-// Inclusive prefix sum over the 64 lanes of the wave (all lanes active).
+// Inclusive prefix sum over the 64 lanes of the wave (all lanes active):
+// DPP row shifts within each 16-lane row, then the row totals (readlane of
+// lanes 15 / 31 / 47) added to the rows after them -- no LDS traffic.
 __device__ __forceinline__ uint32_t wave_scan_add(uint32_t v, uint32_t lane)
 {
-#pragma unroll
-	for (uint32_t d = 1; d < WAVE; d <<= 1) {
-		const uint32_t t = lane_get(v, lane >= d ? lane - d : lane);
-		v += lane >= d ? t : 0u;
-	}
-	return v;
+	v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);   // row_shr:1
+	v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);   // row_shr:2
+	v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);   // row_shr:4
+	v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);   // row_shr:8
+	const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)v, 15);
+	const uint32_t r1 = (uint32_t)__builtin_amdgcn_readlane((int)v, 31);
+	const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)v, 47);
+	const uint32_t row = lane >> 4;
+	return v + (row >= 1u ? r0 : 0u) + (row >= 2u ? r1 : 0u) + (row >= 3u ? r2 : 0u);
 }
-
-// 16-B pieces of the cooperative one's-complement sum in flight per lane
-#ifndef CK_UNROLL
-#define CK_UNROLL 4
-#endif
 
 // Wave-cooperative one's-complement sums of the UDP / TCP payloads of a
 // tile (all 64 lanes active).  Lane f asks for the sum of frame bytes
-// [from, to) of its frame: `cnt` 16-B pieces starting at batch offset `base`
-// (the frame-relative 16-B boundary at or below `from`), with
-// prm = (from - boundary) | (to - boundary) << 4.  The pieces of all lanes
+// [from, to) of its frame: `cnt` 64-B pieces starting at batch offset `base`
+// (the frame-relative 64-B boundary at or below `from`), with
+// prm = (from - boundary) | (to - boundary) << 6.  The pieces of all lanes
 // are numbered in lane order (a wave prefix sum of cnt) and dealt out 64 per
-// round: lane j of a round loads piece g = round base + j, which belongs to
+// round: lane j of a round takes piece g = round base + j, which belongs to
 // the last lane whose first piece number is <= g (binary search over the
-// lanes' first numbers with ds_bpermute).  Consecutive pieces are
-// consecutive bytes of one frame and the frames of a tile are consecutive in
-// the batch, so one load instruction reads ~1 KB of contiguous bytes instead
-// of 16 B from each of 64 frames, and every lane is busy whatever the frame
-// lengths are (the per-lane loop ran every lane for the longest frame of the
-// tile).  Each piece is folded to a 19-bit value congruent to its sum of
-// 16-bit words modulo 0xffff (2^16 == 1), a prefix sum over the round gives
-// each owner its pieces' total as the difference of two prefix values.
-// Returns the lane's own sum (congruent mod 0xffff, < 2^32).
+// lanes' first numbers with ds_bpermute), and reads its 64 bytes with four
+// 16-B loads.  Consecutive pieces are consecutive bytes of one frame and a
+// tile's frames are consecutive in the batch, so a round reads ~4 KB of
+// contiguous bytes, and every lane is busy whatever the frame lengths are
+// (a per-lane loop ran every lane for the longest frame of the tile).
+// Dwords wholly inside [from, to) are summed as they are; the two partial
+// dwords (`from` is even: the upper half of its dword; the bytes of `to`'s
+// dword below it) come from two extra dword loads.  Each piece is folded to a
+// value congruent to its sum of 16-bit words modulo 0xffff (2^16 == 1), and a
+// prefix sum over the round gives each owner its pieces' total as the
+// difference of two prefix values.  Returns the lane's own sum (congruent
+// mod 0xffff, < 2^32).
 __device__ __forceinline__ uint32_t ck_sum_wave(__amdgpu_buffer_rsrc_t rs, uint32_t base,
 						uint32_t prm, uint32_t cnt, uint32_t lane)
 {
@@ -491,76 +496,106 @@ __device__ __forceinline__ uint32_t ck_sum_wave(__amdgpu_buffer_rsrc_t rs, uint3
 	const uint32_t first = incl - cnt;   // number of this lane's first piece
 	const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, WAVE - 1);
 	uint32_t acc = 0;
-	for (uint32_t B = 0; B < total; B += CK_UNROLL * WAVE) {
-		u32x4 v[CK_UNROLL];
-		uint32_t pr[CK_UNROLL], q16[CK_UNROLL];
+	for (uint32_t B = 0; B < total; B += WAVE) {
+		const uint32_t g = B + lane;
+		uint32_t lo = 0;
 #pragma unroll
-		for (uint32_t u = 0; u < CK_UNROLL; ++u) {
-			const uint32_t g = B + u * WAVE + lane;
-			uint32_t lo = 0;
-#pragma unroll
-			for (uint32_t s = WAVE / 2; s >= 1; s >>= 1) {
-				const uint32_t c = lo + s;
-				lo = lane_get(first, c) <= g ? c : lo;
-			}
-			const uint32_t q = g - lane_get(first, lo);
-			pr[u] = lane_get(prm, lo);
-			q16[u] = 16u * q;
-			const uint32_t ob = lane_get(base, lo);
-			v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, g < total ? ob + q16[u] : OOB_OFF,
-								     0, 0);
+		for (uint32_t s = WAVE / 2; s >= 1; s >>= 1) {
+			const uint32_t c = lo + s;
+			lo = lane_get(first, c) <= g ? c : lo;
 		}
+		const uint32_t q = g - lane_get(first, lo);
+		const uint32_t pr = lane_get(prm, lo);
+		const uint32_t ob = lane_get(base, lo) + 64u * q;
+		const bool live = g < total;
+		// the piece's byte window [lb, hb), relative to its start
+		const int32_t lb = (int32_t)(pr & 63u) - (int32_t)(64u * q);
+		const int32_t hb = (int32_t)(pr >> 6) - (int32_t)(64u * q);
+		u32x4 v[4];
 #pragma unroll
-		for (uint32_t u = 0; u < CK_UNROLL; ++u) {
-			const uint32_t from = pr[u] & 15u, to = pr[u] >> 4;
-			uint64_t s = 0;
+		for (int32_t k = 0; k < 4; ++k)
+			v[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, (live && 16 * k < hb) ? ob + 16u * k
+											 : OOB_OFF, 0, 0);
+		const bool ph = live && lb > 0 && (lb & 3) != 0;
+		const bool pt = live && hb < 64 && (hb & 3) != 0;
+		const uint32_t xh = __builtin_amdgcn_raw_buffer_load_b32(
+			rs, ph ? ob + (uint32_t)(lb & ~3) : OOB_OFF, 0, 0);
+		const uint32_t xt = __builtin_amdgcn_raw_buffer_load_b32(
+			rs, pt ? ob + (uint32_t)(hb & ~3) : OOB_OFF, 0, 0);
+		uint64_t s = (uint64_t)(xh >> 16) + (xt & ((1u << (8u * ((uint32_t)hb & 3u))) - 1u));
+		// dword d is wholly inside iff lb <= 4d and 4d + 4 <= hb
+		const uint32_t lo4 = (uint32_t)max(lb, 0);
+		const int32_t sp = hb - 4 - max(lb, 0);   // < 0: no whole dword
 #pragma unroll
-			for (uint32_t j = 0; j < 4; ++j) {
-				const uint32_t qq = q16[u] + 4u * j;
-				const uint32_t lo = from > qq ? min(from - qq, 4u) : 0u;
-				const uint32_t hi = to > qq ? min(to - qq, 4u) : 0u;
-				const uint32_t mhi = hi >= 4u ? ~0u : ((1u << (8u * hi)) - 1u);
-				const uint32_t mlo = lo >= 4u ? ~0u : ((1u << (8u * lo)) - 1u);
-				s += v[u][j] & mhi & ~mlo;
-			}
-			// < 2^18 + 2^16; pieces past the last one (g >= total) read 0
-			const uint32_t r = (uint32_t)(s & 0xffffu) + (uint32_t)(s >> 16);
-			const uint32_t P = wave_scan_add(r, lane);
-			// this lane's pieces in the round: lanes [a, e) of it
-			const uint32_t rb0 = B + u * WAVE;
-			const uint32_t a = first > rb0 ? first - rb0 : 0u;
-			const uint32_t e = min(incl > rb0 ? incl - rb0 : 0u, (uint32_t)WAVE);
-			const uint32_t pe = lane_get(P, e > 0u ? e - 1u : 0u);
-			const uint32_t pa = lane_get(P, a > 0u ? a - 1u : 0u);
-			acc += (e > a) ? pe - (a > 0u ? pa : 0u) : 0u;
+		for (uint32_t d = 0; d < 16; ++d) {
+			const bool in = live && sp >= 0 && (4u * d - lo4) <= (uint32_t)sp;
+			s += in ? v[d >> 2][d & 3u] : 0u;
 		}
+		// < 2^20 + 2^16
+		const uint32_t r = (uint32_t)(s & 0xffffu) + (uint32_t)(s >> 16);
+		const uint32_t P = wave_scan_add(r, lane);
+		// this lane's pieces in the round: lanes [a, e) of it
+		const uint32_t a = first > B ? first - B : 0u;
+		const uint32_t e = min(incl > B ? incl - B : 0u, (uint32_t)WAVE);
+		const uint32_t pe = lane_get(P, e > 0u ? e - 1u : 0u);
+		const uint32_t pa = lane_get(P, a > 0u ? a - 1u : 0u);
+		acc += (e > a) ? pe - (a > 0u ? pa : 0u) : 0u;
 	}
 	return acc;
 }
 
 // CRC-32C part of the SCTP check (odp_packet.c:2112-2131 via
 // _odp_packet_sctp_chksum): over [l4, frame_len) with the 4-byte checksum
-// field at l4 + 8 taken as zero, init ~0, four bytes per step from aligned
-// dword loads of the frame (funnel-shifted when l4 is 2 mod 4), the last
-// 0-3 bytes one at a time.  Returns the finished (inverted) CRC.
+// field at l4 + 8 taken as zero, init ~0, four bytes per step (slicing-by-4)
+// from 16-B loads of the frame (frame-relative 16-B pieces: never past the
+// frame's 16-B rounding, the batch contract), the words funnel-shifted when
+// l4 is 2 mod 4; the last 0-3 bytes one at a time.  Returns the finished
+// (inverted) CRC.
+#ifndef CK_AHEAD
+#define CK_AHEAD 4          // 16-B pieces in flight per lane in sctp_crc
+#endif
 __device__ __forceinline__ uint32_t sctp_crc(const Pkt &k, __amdgpu_buffer_rsrc_t rs, uint32_t boff,
-					     uint32_t l4)
+					     uint32_t l4, const uint32_t *tab)
 {
-	const uint32_t len = k.len, sh = l4 & 3u, n4 = (len - l4) >> 2;
-	uint32_t j = l4 >> 2;
-	uint32_t prev = __builtin_amdgcn_raw_buffer_load_b32(rs, boff + 4u * j, 0, 0);
-	uint32_t crc = 0xffffffffu;
-	for (uint32_t i = 0; i < n4; ++i) {
-		++j;
-		// dword 4j reaches at most 4 - sh bytes past the word: never past the
-		// frame's 16-B rounding (the batch contract)
-		const uint32_t next = __builtin_amdgcn_raw_buffer_load_b32(rs, boff + 4u * j, 0, 0);
-		const uint32_t w = __builtin_amdgcn_alignbyte(next, prev, sh);
-		crc = crc32c_u32(crc, i == 2u ? 0u : w);
-		prev = next;
+	const uint32_t len = k.len, sh = l4 & 3u, j0 = l4 >> 2, n4 = (len - l4) >> 2;
+	// word i (bytes l4 + 4i ..) = alignbyte(dword j0 + i + 1, dword j0 + i)
+	uint32_t crc = 0xffffffffu, prev = 0u;
+	const uint32_t jend = j0 + n4;   // last low dword index + 1
+	// pieces are loaded CK_AHEAD ahead of the one the CRC steps consume (the
+	// steps are a dependent chain of LDS lookups: without the lookahead
+	// every piece would wait a full memory latency); a piece starting at or
+	// past frame_len is not loaded (at frame_len, l4 = 0 mod 4 and frame_len
+	// = 0 mod 16: it only feeds the last word's unused high half)
+	const uint32_t q0 = (j0 >> 2) << 2;
+	u32x4 nx[CK_AHEAD];
+#pragma unroll
+	for (uint32_t i = 0; i < CK_AHEAD; ++i) {
+		const uint32_t qi = q0 + 4u * i;
+		nx[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (qi <= jend && 4u * qi < len)
+								      ? boff + 4u * qi : OOB_OFF, 0, 0);
+	}
+	for (uint32_t q = q0; q <= jend; q += 4u) {
+		const u32x4 v = nx[0];
+#pragma unroll
+		for (uint32_t i = 0; i + 1 < CK_AHEAD; ++i)
+			nx[i] = nx[i + 1];
+		{
+			const uint32_t qn = q + 4u * CK_AHEAD;
+			nx[CK_AHEAD - 1] = __builtin_amdgcn_raw_buffer_load_b128(
+				rs, (qn <= jend && 4u * qn < len) ? boff + 4u * qn : OOB_OFF, 0, 0);
+		}
+#pragma unroll
+		for (uint32_t t = 0; t < 4; ++t) {
+			// word whose low dword is q + t - 1 (its high dword is v[t])
+			const uint32_t lo = q + t - 1u;
+			const uint32_t w = __builtin_amdgcn_alignbyte(v[t], prev, sh);
+			const bool in = q + t >= 1u && lo >= j0 && lo < jend;
+			crc = in ? crc32c_u32(tab, crc, lo - j0 == 2u ? 0u : w) : crc;
+			prev = v[t];
+		}
 	}
 	for (uint32_t o = l4 + 4u * n4; o < len; ++o)
-		crc = crc32c_u8(crc, rb(k, o));
+		crc = crc32c_u8(tab, crc, rb(k, o));
 	return ~crc;
 }
 
@@ -575,7 +610,7 @@ __device__ __forceinline__ uint32_t sctp_crc(const Pkt &k, __amdgpu_buffer_rsrc_
 // lane of the wave active.
 __device__ __forceinline__ void l4_chksum(const Pkt &k, Parsed &p, uint32_t opt,
 					  __amdgpu_buffer_rsrc_t rs, uint32_t boff, uint32_t lane,
-					  bool valid)
+					  bool valid, const uint32_t *crc_tab)
 {
 	const uint32_t f = p.flags, len = k.len, l3 = p.l3, l4 = p.l4;
 	const bool go = valid && p.ret == 0 && !(f & F_IPFRAG);
@@ -599,17 +634,17 @@ __device__ __forceinline__ void l4_chksum(const Pkt &k, Parsed &p, uint32_t opt,
 			else              // odp_cpu_to_be_16(frame_len - l4), IPPROTO_TCP << 8
 				s += (((len - l4) & 0xffu) << 8) + (((len - l4) >> 8) & 0xffu) + (6u << 8);
 			// the parse guarantees l4 + 8 <= len (UDP) / l4 + 20 <= len (TCP)
-			const uint32_t p0 = l4 & ~15u;
-			cnt = (len - p0 + 15u) >> 4;
+			const uint32_t p0 = l4 & ~63u;
+			cnt = (len - p0 + 63u) >> 6;
 			base = boff + p0;
-			prm = (l4 - p0) | ((len - p0) << 4);
+			prm = (l4 - p0) | ((len - p0) << 6);
 		}
 		s += ck_sum_wave(rs, base, prm, cnt, lane);
 	}
 	bool bad = sum && ck_finalize(s) != 0xffffu;   // ~sum != 0
 	if (__ballot(kind == 3u) != 0ull) {
 		if (kind == 3u)
-			bad = sctp_crc(k, rs, boff, l4) != r32(k, l4 + 8u);
+			bad = sctp_crc(k, rs, boff, l4, crc_tab) != r32(k, l4 + 8u);
 	}
 	if (kind != 0u) {
 		p.flags |= F_L4CK_DONE;
@@ -1032,6 +1067,9 @@ enum { DH_MAGIC = 0, DH_NCOS, DH_DEFAULT, DH_ERROR, DH_DEFAULT_VALID, DH_USED, D
 #define BVF_TAG 8u              // merged UDP/TCP port class: protocol tag at bit cr(3)
 #define BV_EMPTY 0xFFFFFFFFu
 #define BV_NONE 0xFFFFFFFEu
+// direct blocks: a slot value / miss word is the rule's result word
+// (dst | leaf << 8 | mark << 16) with this bit set; 0 / BV_EMPTY: no rule
+#define BV_RES_VALID 0x200u
 
 // Classification block of a CoS ("BV" block for historical reasons), used
 // when its rules fall into at most BV_MAX_CLS key classes (a key class is one
@@ -1235,13 +1273,20 @@ __device__ __forceinline__ void bv_eval(const D &blk, T H, bool act, const Pkt &
 	const uint32_t mode = FM >= 0 ? (uint32_t)FM : hb(0), ncls = hb(1), res = hb(2);
 	uint32_t first = BV_NONE;
 	if (mode == 0u) {
-		// direct: one class, the slot holds 1 + the first live rule of its
-		// key (BV_EMPTY: none); a miss takes the block's "no term" rule
+		// direct: one class, the slot holds the result word of the first
+		// live rule of its key (BV_EMPTY: none); a miss takes the block's
+		// "no term" rule (0: none)
 		const D cr = blk.at(8u);
 		uint32_t key[4];
 		const bool present = bv_key(cr, k, p, x, key);
 		const uint32_t val = bv_lookup(cr, H, key, act && present);
-		first = val != 0u ? (val == BV_EMPTY ? BV_NONE : val - 1u) : cr(2);
+		const uint32_t rw = val != 0u ? (val == BV_EMPTY ? 0u : val) : cr(2);
+		const bool h = act && rw != 0u;
+		nxt = h ? (rw & 0xffu) : nxt;
+		nleaf = h ? ((rw >> 8) & 1u) : nleaf;
+		nmark = h ? (rw >> 16) : nmark;
+		hit = h ? 1u : hit;
+		return;
 	} else if (mode == 2u) {
 		// bitmap: AND of the classes' 32-bit rows and the alive row
 		uint32_t acc = hb(4);
@@ -1629,6 +1674,7 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 	__shared__ uint32_t s_win[NW * RS * WROWS];
 	__shared__ uint32_t s_cnt[MAX_STATS_COS];
 	__shared__ uint32_t s_l4[256];
+	__shared__ uint32_t s_crc[CK ? 1024 : 1];   // CRC-32C slicing tables (pktin options)
 
 	const uint32_t lane = threadIdx.x & (WAVE - 1);
 	const uint32_t wave = threadIdx.x >> 6;
@@ -1716,6 +1762,10 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 	}
 	for (uint32_t i = threadIdx.x; i < 256u; i += NW * WAVE)
 		s_l4[i] = c_l4tab.v[i];
+	if constexpr (CK) {
+		for (uint32_t i = threadIdx.x; i < 1024u; i += NW * WAVE)
+			s_crc[i] = c_crc32c.t[i >> 8][i & 0xffu];
+	}
 	for (uint32_t r = WIN / 4; r < WROWS; ++r)
 		W[r * RS + lane] = 0u;   // pad / zero rows: always zero
 	__syncthreads();
@@ -1790,24 +1840,46 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 					p = parse_packet(k, 0u);
 			}
 		} else {
-			// pktin options.  Checksum options: the general parser for every
-			// lane, then the L4 checksums (whole frames from HBM, the wave
-			// cooperating).  Drop options alone act only on lanes whose
-			// parse reports an error, so the fast parse stands for every
-			// other lane and only those are re-parsed with the options.
-			if (a.opt & (OPT_IPV4_CK | OPT_L4_CK)) {
-				p = parse_packet(k, a.opt);
-			} else {
-				bool slow;
-				p = parse_fast(k, s_l4, slow);
-				slow = slow || p.err != 0u;
-				if (__ballot(slow) != 0ull) {
-					if (slow)
-						p = parse_packet(k, a.opt);
+			// pktin options.  The fast parse stands for every lane whose
+			// result the options do not change; parse_packet(opt) re-parses
+			// the others: lanes with a parse error (drop options), a bad IPv4
+			// header checksum, or a zero UDP checksum (the parse_udp rule).
+			// A good IPv4 header checksum only adds l3_chksum_done.  Then
+			// the L4 checksums (whole frames from HBM, the wave cooperating).
+			bool slow;
+			p = parse_fast(k, s_l4, slow);
+			p.udp_zero = 0;
+			slow = slow || p.err != 0u;
+			if (a.opt & OPT_IPV4_CK) {
+				// odp_parse.c:134-141: sum over the ihl * 4 header bytes
+				const bool v4 = !slow && (p.flags & F_IPV4) != 0u;
+				if (__ballot(v4) != 0ull) {
+					if (v4) {
+						const uint32_t ihl = rb(k, p.l3) & 0xfu;
+						uint64_t sum = 0;
+						for (uint32_t i = 0; i < ihl; ++i)
+							sum += r32(k, p.l3 + 4u * i);
+						if (ck_finalize(sum) != 0xffffu)
+							slow = true;
+						else
+							p.flags |= F_L3CK_DONE;
+					}
 				}
 			}
+			if (a.opt & OPT_UDP_CK) {
+				const bool u = !slow && (p.flags & F_UDP) != 0u && !(p.flags & F_IPFRAG) &&
+					       p.ret == 0;
+				if (__ballot(u) != 0ull) {
+					if (u && r16(k, p.l4 + 6u) == 0u)
+						slow = true;
+				}
+			}
+			if (__ballot(slow) != 0ull) {
+				if (slow)
+					p = parse_packet(k, a.opt);
+			}
 			if (a.opt & OPT_L4_CK)
-				l4_chksum(k, p, a.opt, rs, my_off, lane, valid);
+				l4_chksum(k, p, a.opt, rs, my_off, lane, valid, s_crc);
 		}
 		const Fields x = fields_of(k, p);
 		{
@@ -1820,7 +1892,7 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 #ifdef DIAG_FORCE_HI
 			want_hi = true;
 #else
-			want_hi = a.opt != 0u || __ballot(valid && my_len > 64u && need > 64u) != 0ull;
+			want_hi = __ballot(valid && my_len > 64u && need > 64u) != 0ull;
 #endif
 			saw_hi = saw_hi || want_hi;
 		}

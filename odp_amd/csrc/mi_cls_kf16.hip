@@ -1,0 +1,30 @@
+// mi_cls_kf16.hip -- flat-program instantiations of mi_cls_kernel for the
+// 16-wave block shape (see mi_cls_kf.hip).
+#include "mi_cls_dev.h"
+
+template <int NW>
+static int launch_fm(int fm, unsigned grid, size_t dyn, hipStream_t st, const KArgs &a)
+{
+	switch (fm) {
+	case 0:
+		hipLaunchKernelGGL((mi_cls_kernel<true, false, NW, 0>), dim3(grid), dim3(NW * WAVE), dyn, st, a);
+		break;
+	case 2:
+		hipLaunchKernelGGL((mi_cls_kernel<true, false, NW, 2>), dim3(grid), dim3(NW * WAVE), dyn, st, a);
+		break;
+	case 3:
+		hipLaunchKernelGGL((mi_cls_kernel<true, false, NW, 3>), dim3(grid), dim3(NW * WAVE), dyn, st, a);
+		break;
+	case 4:
+		hipLaunchKernelGGL((mi_cls_kernel<true, false, NW, 4>), dim3(grid), dim3(NW * WAVE), dyn, st, a);
+		break;
+	default:
+		return -EINVAL;
+	}
+	return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+int mi_cls_launch_flat16(int fm, unsigned grid, size_t dyn, hipStream_t st, const KArgs &a)
+{
+	return launch_fm<16>(fm, grid, dyn, st, a);
+}
