@@ -551,8 +551,16 @@ static bool build_bv(const mi_cos_t *cs, const mi_rule_t *rs, const mi_term_t *t
 		// single-candidate records, 16-B aligned, RW = 1 + ncls rounded up
 		// to 4 words: w0 = constrained-class mask (bit 31: never holds),
 		// w[1 + c] = what class c must be: the masked value (one-word
-		// classes) or the key id (longer keys)
-		const uint32_t RW = (1u + ncls + 3u) & ~3u;
+		// classes) or the key id (longer keys).  Compact form (more than 3
+		// classes, but no alive rule constrains more than 3): RW = 4, the
+		// values of the constrained classes in class order (w[1 + j] for the
+		// j-th set bit of the mask) -- a quarter to a half of the bytes, so
+		// larger rule sets keep their hot region in LDS
+		bool compact = ncls > 3u;
+		for (uint32_t r = 0; r < nrules && compact; ++r)
+			if (alive[r] && __builtin_popcount(tmask[r]) > 3)
+				compact = false;
+		const uint32_t RW = compact ? 4u : (1u + ncls + 3u) & ~3u;
 		align4();
 		blk[4] = base + (uint32_t)blk.size();
 		blk[5] = RW;
@@ -566,10 +574,11 @@ static bool build_bv(const mi_cos_t *cs, const mi_rule_t *rs, const mi_term_t *t
 			std::vector<uint32_t> rec(RW, 0);
 			if (alive[r]) {
 				rec[0] = tmask[r];
+				uint32_t j = 0;
 				for (uint32_t c = 0; c < ncls; ++c)
 					if ((tmask[r] >> c) & 1u)
-						rec[1 + c] = cls_list[c].nkey == 1u ? want[r][c][0]
-										 : kid[c][want[r][c]];
+						rec[1 + (compact ? j++ : c)] = cls_list[c].nkey == 1u
+							? want[r][c][0] : kid[c][want[r][c]];
 			} else {
 				rec[0] = 0x80000000u;
 			}

@@ -1168,12 +1168,34 @@ struct DescU {
 		return DescV{ *(const __attribute__((address_space(4))) u32x16 *)(p + o) };
 	}
 };
+// 16-byte read of the hot region (LDS: ds_read_b128, HBM: global dwordx4);
+// i is a multiple of 4 (hot-region blocks, buckets and rows are 16-B aligned)
+__device__ __forceinline__ u32x4 ld4(lword_t H, uint32_t i)
+{
+	return *(const __attribute__((address_space(3))) u32x4 *)(H + i);
+}
+__device__ __forceinline__ u32x4 ld4(gword_t H, uint32_t i)
+{
+	return *(const __attribute__((address_space(1))) u32x4 *)(H + i);
+}
+
+// Per-lane descriptor in the hot region: words on demand, or 16 words at
+// once with four 16-B reads (vec: block headers and class records are
+// 16-B aligned), instead of one dependent read per word used.
 template <typename T> struct DescL {
 	T p;
 	uint32_t b;
 	__device__ __forceinline__ uint32_t operator()(uint32_t i) const { return p[b + i]; }
 	__device__ __forceinline__ DescL at(uint32_t o) const { return DescL{ p, b + o }; }
-	__device__ __forceinline__ DescL vec(uint32_t o) const { return at(o); }
+	__device__ __forceinline__ DescV vec(uint32_t o) const
+	{
+		const u32x4 q0 = ld4(p, b + o), q1 = ld4(p, b + o + 4u), q2 = ld4(p, b + o + 8u),
+			    q3 = ld4(p, b + o + 12u);
+		DescV d;
+		d.v = u32x16{ q0[0], q0[1], q0[2], q0[3], q1[0], q1[1], q1[2], q1[3],
+			      q2[0], q2[1], q2[2], q2[3], q3[0], q3[1], q3[2], q3[3] };
+		return d;
+	}
 };
 
 // Key of a packet for one class: the masked field the class's terms
@@ -1210,17 +1232,6 @@ __device__ __forceinline__ bool bv_key(const D &cr, const Pkt &k, const Parsed &
 		}
 	}
 	return present;
-}
-
-// 16-byte read of the hot region (LDS: ds_read_b128, HBM: global dwordx4);
-// i is a multiple of 4 (hot-region blocks, buckets and rows are 16-B aligned)
-__device__ __forceinline__ u32x4 ld4(lword_t H, uint32_t i)
-{
-	return *(const __attribute__((address_space(3))) u32x4 *)(H + i);
-}
-__device__ __forceinline__ u32x4 ld4(gword_t H, uint32_t i)
-{
-	return *(const __attribute__((address_space(1))) u32x4 *)(H + i);
 }
 
 // Two-choice cuckoo lookup (both candidate buckets read at once, no probe
@@ -1276,7 +1287,7 @@ __device__ __forceinline__ void bv_eval(const D &blk, T H, bool act, const Pkt &
 		// direct: one class, the slot holds the result word of the first
 		// live rule of its key (BV_EMPTY: none); a miss takes the block's
 		// "no term" rule (0: none)
-		const D cr = blk.at(8u);
+		const auto cr = blk.vec(8u);
 		uint32_t key[4];
 		const bool present = bv_key(cr, k, p, x, key);
 		const uint32_t val = bv_lookup(cr, H, key, act && present);
@@ -1374,12 +1385,26 @@ __device__ __forceinline__ void bv_eval(const D &blk, T H, bool act, const Pkt &
 						q2 = ld4(H, ra + 8u);
 					const uint32_t tm = q0[0];
 					bool ok = (tm >> 31) == 0u;
+					if (rw == 4u && ncls > 3u) {
+						// compact record: the constrained classes' values
+						// in class order
 #pragma unroll
-					for (uint32_t c2 = 0; c2 < BV_MAX_CLS; ++c2) {
-						if (c2 < ncls) {
-							const uint32_t w = c2 < 3u ? q0[1 + c2] : (c2 < 7u ? q1[c2 - 3u] : q2[0]);
-							const bool need = (tm >> c2) & 1u;
-							ok = ok && (!need || (((prm >> c2) & 1u) && cmpv[c2] == w));
+						for (uint32_t c2 = 0; c2 < BV_MAX_CLS; ++c2) {
+							if (c2 < ncls) {
+								const uint32_t j = (uint32_t)__builtin_popcount(tm & ((1u << c2) - 1u));
+								const uint32_t w = j == 0u ? q0[1] : (j == 1u ? q0[2] : q0[3]);
+								const bool need = (tm >> c2) & 1u;
+								ok = ok && (!need || (((prm >> c2) & 1u) && cmpv[c2] == w));
+							}
+						}
+					} else {
+#pragma unroll
+						for (uint32_t c2 = 0; c2 < BV_MAX_CLS; ++c2) {
+							if (c2 < ncls) {
+								const uint32_t w = c2 < 3u ? q0[1 + c2] : (c2 < 7u ? q1[c2 - 3u] : q2[0]);
+								const bool need = (tm >> c2) & 1u;
+								ok = ok && (!need || (((prm >> c2) & 1u) && cmpv[c2] == w));
+							}
 						}
 					}
 					first = (tr && ok) ? c1 - 1u : first;

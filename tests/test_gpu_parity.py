@@ -262,3 +262,22 @@ def test_parser_frames_gpu(built, gpu):
     b = pg.batch_from_frames([f for _, f in frames])
     got = both([R.cos("d", queue=1), ("default", 0)], b, what="parser frames")
     assert np.all(got["outcome"] == R.OUT_ENQ)
+
+
+@pytest.mark.parametrize("four_terms", [False, True])
+def test_single_candidate_record_forms(built, gpu, four_terms):
+    """Single-candidate engine records: config 4's 1024 rules constrain at
+    most 3 of their 7 key classes (compact 16-B records); one extra rule
+    with 4 terms forces the full per-class layout.  Both == oracle."""
+    from odp_amd.cls import Classifier
+    b, prog = R.config4(30_000)
+    if four_terms:
+        terms = [R.t_ip4(R.PMR_SIP_ADDR, "10.1.5.0", 24), R.t_u8(R.PMR_IPPROTO, pg.IPPROTO_UDP),
+                 R.t_be16(R.PMR_UDP_DPORT, 1010), R.t_ip4(R.PMR_DIP_ADDR, "192.168.0.0", 16)]
+        at = next(i for i, op in enumerate(prog) if op[0] == "pmr") + 3
+        prog = prog[:at] + [("pmr", terms, 0, 5, 9)] + prog[at:]
+    c = Classifier(gpu=0)
+    c.apply(prog)
+    assert c.program_info()["cand1"] == 1
+    c.close()
+    both(prog, b, what=f"config4 four_terms={four_terms}")
