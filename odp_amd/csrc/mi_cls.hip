@@ -195,6 +195,14 @@ static uint32_t encode_term(const mi_term_t &t, uint32_t *w)
 	return n;
 }
 
+// key words a term kind reads (encode_term's nw)
+static uint32_t kind_words(uint32_t kind, uint32_t size)
+{
+	if (kind == MI_K_CUSTOM_FRAME || kind == MI_K_CUSTOM_L3)
+		return (size + 3u) / 4u;
+	return (kind == MI_K_SIP6 || kind == MI_K_DIP6) ? 4u : (kind == MI_K_DMAC ? 2u : 1u);
+}
+
 // ---- bit-vector block construction (host) ----
 struct ClassKey {
 	uint32_t kind, nkey, offset, size, mask[4];
@@ -229,7 +237,7 @@ static uint32_t host_bucket(uint32_t x, uint32_t mult, uint32_t nb)
 
 // Two-choice cuckoo table over `keys`: every key sits in a slot of bucket
 // b1 or b2 (a lookup reads both buckets at once, no probe loop).  bsz slots
-// per bucket: 2 for one-word keys (a 16-B bucket, load <= 80 %), 1 for
+// per bucket: 2 for one-word keys (a 16-B bucket, load <= 87.5 %), 1 for
 // longer keys (load <= 45 %).  Returns the slot (bucket * bsz + j) of every
 // key, the bucket count and the multipliers used.
 static bool cuckoo_place(const std::vector<Key4> &keys, uint32_t nk, uint32_t bsz, uint32_t &nb_out,
@@ -239,8 +247,9 @@ static bool cuckoo_place(const std::vector<Key4> &keys, uint32_t nk, uint32_t bs
 	std::vector<uint32_t> fold(n);
 	for (uint32_t i = 0; i < n; ++i)
 		fold[i] = nk == 1 ? keys[i][0] : host_bv_fold(keys[i]);
-	// load <= 80 % with 2-slot buckets, <= 45 % otherwise
-	uint32_t nb = bsz == 2 ? (n * 5 + 7) / 8 : (n * 20 + 8) / 9 + 1;
+	// load <= 87.5 % with 2-slot buckets (below the ~89.7 % two-choice
+	// threshold; a failed placement grows the table), <= 45 % otherwise
+	uint32_t nb = bsz == 2 ? (n * 4 + 6) / 7 : (n * 20 + 8) / 9 + 1;
 	if (nb < 1)
 		nb = 1;
 	uint64_t rng = 0x9E3779B97F4A7C15ull ^ ((uint64_t)n << 17);
@@ -329,6 +338,10 @@ static bool class_of(const mi_term_t &t, ClassKey &ck)
 	}
 	for (uint32_t i = 0; i < 4; ++i)
 		ck.mask[i] = i < ck.nkey ? eff_mask(t, i) : 0;
+	// trailing key words the mask clears are not part of the key (an IPv6
+	// /64 prefix is a two-word key: half the key reads, 16-B table slots)
+	while (ck.nkey > 1 && ck.mask[ck.nkey - 1] == 0)
+		--ck.nkey;
 	// UDP and TCP port terms read the same bytes (the raw port word at l4)
 	// under different gates: one class for both, the protocol carried in
 	// two key bits the mask leaves free (tag 1 UDP, 2 TCP; port masks are
@@ -387,7 +400,7 @@ static Key4 class_value(const mi_term_t &t, const ClassKey &ck)
 //    with no classified term (it matches everything); a candidate holds iff
 //    its record's key ids equal the packet's, and the smallest one wins.
 static bool build_bv(const mi_cos_t *cs, const mi_rule_t *rs, const mi_term_t *ts, uint32_t nrules,
-		     uint32_t base, std::vector<uint32_t> &blk)
+		     uint32_t base, std::vector<uint32_t> &blk, std::array<uint32_t, 16> &shared)
 {
 	std::map<ClassKey, uint32_t> cls;
 	std::vector<ClassKey> cls_list;
@@ -424,6 +437,12 @@ static bool build_bv(const mi_cos_t *cs, const mi_rule_t *rs, const mi_term_t *t
 			}
 			const uint32_t c = cls[ck];
 			const Key4 v = class_value(tm, ck);
+			// a value bit under a zero mask word (trimmed from the key) can
+			// never be matched; values are pre-masked by the control plane,
+			// this guards other producers of the table
+			for (uint32_t i = ck.nkey; i < 4; ++i)
+				if ((kind_words(tm.kind, tm.size) > i) && tm.value[i] != 0u)
+					ok = false;
 			if (((tmask[r] >> c) & 1u) && want[r][c] != v)
 				ok = false;   // two terms of one class with different values
 			tmask[r] |= 1u << c;
@@ -477,8 +496,13 @@ static bool build_bv(const mi_cos_t *cs, const mi_rule_t *rs, const mi_term_t *t
 	for (uint32_t r = 0; r < nrules && wc_first == BV_NONE; ++r)
 		if (alive[r] && tmask[r] == 0u)
 			wc_first = r;
-	// header (8) | classes (16 each) | results | [records] | per class: table [, lists]
-	blk.assign(8 + BV_CLS_WORDS * ncls, 0);
+	// header (8) | classes (16 each) | results | [records] | per class: table [, lists].
+	// Direct blocks: header (8: mode, 1, shared class record, miss result,
+	// bucket count, table, m1, m2) | table; their 16-word class record
+	// (`shared`, the block-specific words zero) is stored once per distinct
+	// record in the hot region by assemble(), which patches word 2
+	blk.assign(mode == 0u ? 8u : 8u + BV_CLS_WORDS * ncls, 0);
+	shared.fill(0u);
 	blk[0] = mode;
 	blk[1] = ncls;
 	blk[3] = wc_first;
@@ -638,20 +662,37 @@ static bool build_bv(const mi_cos_t *cs, const mi_rule_t *rs, const mi_term_t *t
 		if (!cuckoo_place(keys, ck.nkey, bsz, nb, m1, m2, slot_of))
 			return false;
 		const uint32_t cbase = 8 + BV_CLS_WORDS * c;
-		const uint32_t SW = ck.nkey + 1u;   // slot: key words, value
-		blk[cbase + 0] = ck.kind;
-		blk[cbase + 1] = ck.nkey;
+		auto setc = [&](uint32_t w, uint32_t v) {
+			if (mode == 0u)
+				shared[w] = v;
+			else
+				blk[cbase + w] = v;
+		};
+		// slot: key words, value; one-word keys 2 words (two slots per 16-B
+		// bucket), 2-3-word keys one 16-B slot, 4-word keys 32 B
+		const uint32_t SW = bsz == 2u ? 2u : (ck.nkey <= 3u ? 4u : 8u);
+		setc(0, ck.kind);
+		setc(1, ck.nkey);
 		const uint32_t fl0 = mode == 0u ? first_live(c, nullptr) : 0u;
 		const uint32_t miss = mode == 0u ? (fl0 == BV_NONE ? 0u : res_word(fl0) | BV_RES_VALID)
 			: (mode == 2u ? row_of(c, nullptr) : (mode == 3u ? base + rows_at + 4u * miss_id[c] : 0u));
-		blk[cbase + 2] = miss;
-		blk[cbase + 3] = ck.offset;
-		blk[cbase + 4] = ck.size;
+		if (mode == 0u)
+			blk[3] = miss;
+		else
+			blk[cbase + 2] = miss;
+		setc(3, ck.offset);
+		setc(4, ck.size);
 		for (int i = 0; i < 4; ++i)
-			blk[cbase + 5 + i] = ck.mask[i];
-		blk[cbase + 9] = nb;
-		blk[cbase + 11] = m1;
-		blk[cbase + 12] = m2;
+			setc(5 + i, ck.mask[i]);
+		if (mode == 0u) {
+			blk[4] = nb;
+			blk[6] = m1;
+			blk[7] = m2;
+		} else {
+			blk[cbase + 9] = nb;
+			blk[cbase + 11] = m1;
+			blk[cbase + 12] = m2;
+		}
 		{
 			const bool special = ck.kind == MI_K_LEN || ck.kind == MI_K_PCP0 ||
 					     ck.kind == MI_K_DSCP;
@@ -666,13 +707,15 @@ static bool build_bv(const mi_cos_t *cs, const mi_rule_t *rs, const mi_term_t *t
 			const uint32_t fl = (special ? BVF_SPECIAL : 0u) |
 				((ck.kind == MI_K_CUSTOM_FRAME || ck.kind == MI_K_CUSTOM_L3) ? BVF_CUSTOM : 0u) |
 				(ck.kind == MI_K_CUSTOM_L3 ? BVF_L3 : 0u) | (ck.kind == K_L4PORT ? BVF_TAG : 0u);
-			blk[cbase + BVC_AO] = d.add | (d.alt << 16);
-			blk[cbase + BVC_DESC] = (gate & 0xffffffu) | (d.base << 24) | (ac << 26) | (fl << 28);
+			setc(BVC_AO, d.add | (d.alt << 16));
+			setc(BVC_DESC, (gate & 0xffffffu) | (d.base << 24) | (ac << 26) | (fl << 28));
 		}
-		if (bsz == 2)
-			align4();   // 16-B buckets
+		align4();   // 16-B buckets / slots
 		const uint32_t tbl_off = (uint32_t)blk.size();
-		blk[cbase + 10] = base + tbl_off;
+		if (mode == 0u)
+			blk[5] = base + tbl_off;
+		else
+			blk[cbase + 10] = base + tbl_off;
 		// empty slots keep key words 0 and value 0: a miss (every stored
 		// value is non-zero)
 		blk.resize(blk.size() + (size_t)nb * bsz * SW, 0);
@@ -738,17 +781,30 @@ static int assemble(const void *tbl, uint32_t **out, size_t *out_words)
 		c[C_REC0] = cs[s].rule_begin;
 	}
 	if (!getenv("MI_CLS_NO_BV")) {
+		// direct blocks' class records, one copy per distinct record
+		std::map<std::array<uint32_t, 16>, std::vector<uint32_t>> shared_users;
 		for (uint32_t s = 0; s < h->num_cos; ++s) {
 			if (!cs[s].valid || cs[s].num_rules == 0)
 				continue;
 			std::vector<uint32_t> blk;
+			std::array<uint32_t, 16> shared;
 			while (hot.size() & 3u)   // blocks start 16-B aligned (16-B row / bucket reads)
 				hot.push_back(0);
 			const uint32_t base = (uint32_t)hot.size();
-			if (build_bv(cs, rs + cs[s].rule_begin, ts, cs[s].num_rules, base, blk)) {
+			if (build_bv(cs, rs + cs[s].rule_begin, ts, cs[s].num_rules, base, blk, shared)) {
 				hot[COS_WORDS * s + C_BV] = base;
 				hot.insert(hot.end(), blk.begin(), blk.end());
+				if (blk[0] == 0u)
+					shared_users[shared].push_back(base);
 			}
+		}
+		for (auto &kv : shared_users) {
+			while (hot.size() & 3u)
+				hot.push_back(0);
+			const uint32_t at = (uint32_t)hot.size();
+			hot.insert(hot.end(), kv.first.begin(), kv.first.end());
+			for (uint32_t b : kv.second)
+				hot[b + 2] = at;
 		}
 	}
 	// cold region: 16-word rule records (+ ext terms appended after them)

@@ -49,7 +49,7 @@
 #ifndef WIN
 #define WIN 96             // staged header window, bytes (96 or 128)
 #endif
-#define WROWS (WIN / 4 + 3)     // LDS dword rows per wave window (+3 zero rows)
+#define WROWS (WIN / 4 + 1)     // LDS dword rows per wave window (+1 zero row)
 #define RS 66                   // LDS row stride of a window, dwords (see load_window)
 #define NPIECE (WIN / 16)       // 16-B pieces per window
 #ifndef MIN_WAVES_PER_EU
@@ -139,11 +139,12 @@ __device__ __forceinline__ uint32_t rb(const Pkt &k, uint32_t o)
 
 // 4 bytes starting at byte offset o, little-endian (== the reference's raw
 // load).  The LDS read is unconditional (row index clamped into the window
-// and its zero rows), so lanes do not diverge; a wave-uniform branch fixes up
+// and its zero row: a lane whose 4 bytes lie in the window reads rows <=
+// WIN/4), so lanes do not diverge; a wave-uniform branch fixes up
 // the lanes whose 4 bytes reach past the staged window (bytes from HBM).
 __device__ __forceinline__ uint32_t r32(const Pkt &k, uint32_t o)
 {
-	const uint32_t i = min(o >> 2, (uint32_t)(WIN / 4 + 1));
+	const uint32_t i = min(o >> 2, (uint32_t)(WIN / 4 - 1));
 	uint32_t v = __builtin_amdgcn_alignbyte(k.w[(i + 1) * RS], k.w[i * RS], o & 3u);
 	const bool far = o + 4u > k.win;
 	if (__ballot(far) != 0ull) {
@@ -1160,13 +1161,17 @@ struct DescV {
 };
 struct DescU {
 	cword_t p;
+	cword_t h;              // start of the hot region (root())
 	__device__ __forceinline__ uint32_t operator()(uint32_t i) const { return p[i]; }
-	__device__ __forceinline__ DescU at(uint32_t o) const { return DescU{ p + o }; }
-	// 16 words at o, loaded at once (o: compile-time word offset)
+	__device__ __forceinline__ DescU at(uint32_t o) const { return DescU{ p + o, h }; }
+	// 16 words at o, loaded at once
 	__device__ __forceinline__ DescV vec(uint32_t o) const
 	{
 		return DescV{ *(const __attribute__((address_space(4))) u32x16 *)(p + o) };
 	}
+	__device__ __forceinline__ DescV hdr() const { return vec(0u); }
+	// 16 words at hot-region word o (a direct block's shared class record)
+	__device__ __forceinline__ DescV root(uint32_t o) const { return DescU{ h + o, h }.vec(0u); }
 };
 // 16-byte read of the hot region (LDS: ds_read_b128, HBM: global dwordx4);
 // i is a multiple of 4 (hot-region blocks, buckets and rows are 16-B aligned)
@@ -1194,6 +1199,16 @@ template <typename T> struct DescL {
 		DescV d;
 		d.v = u32x16{ q0[0], q0[1], q0[2], q0[3], q1[0], q1[1], q1[2], q1[3],
 			      q2[0], q2[1], q2[2], q2[3], q3[0], q3[1], q3[2], q3[3] };
+		return d;
+	}
+	__device__ __forceinline__ DescV root(uint32_t o) const { return DescL{ p, o }.vec(0u); }
+	// the 8-word block header
+	__device__ __forceinline__ DescV hdr() const
+	{
+		const u32x4 q0 = ld4(p, b), q1 = ld4(p, b + 4u);
+		DescV d;
+		d.v = u32x16{ q0[0], q0[1], q0[2], q0[3], q1[0], q1[1], q1[2], q1[3],
+			      0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u };
 		return d;
 	}
 };
@@ -1240,11 +1255,11 @@ __device__ __forceinline__ bool bv_key(const D &cr, const Pkt &k, const Parsed &
 // bucket.  An empty slot has key words 0 and value 0, and a key sits in at
 // most one slot, so OR-ing the values of the slots whose key words equal the
 // packet's gives the hit's value, or 0 on a miss.
-template <typename D, typename T>
-__device__ __forceinline__ uint32_t bv_lookup(const D &cr, T H, const uint32_t key[4], bool act)
+template <typename T>
+__device__ __forceinline__ uint32_t bv_probe(T H, const uint32_t key[4], bool act, uint32_t nk,
+					     uint32_t ns, uint32_t tbl, uint32_t m1, uint32_t m2)
 {
 	// ns = bucket count
-	const uint32_t nk = cr(1), ns = cr(9), tbl = cr(10), m1 = cr(11), m2 = cr(12);
 	uint32_t val = 0;
 	if (nk == 1u) {
 		// one-word keys (the common case): bv_fold with zero upper words
@@ -1254,18 +1269,33 @@ __device__ __forceinline__ uint32_t bv_lookup(const D &cr, T H, const uint32_t k
 		      (b2[0] == key[0] ? b2[1] : 0u) | (b2[2] == key[0] ? b2[3] : 0u);
 		return act ? val : 0u;
 	}
+	// longer keys: one slot per bucket, 16 B (2-3 key words, value) or 32 B
+	// (4 key words, value): one or two 16-B reads per bucket
 	const uint32_t f = bv_fold(key);
-	const uint32_t sw = nk + 1u;
 #pragma unroll
 	for (uint32_t s = 0; s < 2; ++s) {
-		const uint32_t a = tbl + bv_bucket(f, s ? m2 : m1, ns) * sw;
-		bool e = H[a] == key[0] && H[a + 1] == key[1];
-		if (nk > 2)
-			e = e && H[a + 2] == key[2] && H[a + 3] == key[3];
-		const uint32_t v = H[a + nk];
+		const uint32_t b = bv_bucket(f, s ? m2 : m1, ns);
+		uint32_t v;
+		bool e;
+		if (nk <= 3u) {
+			const u32x4 q = ld4(H, tbl + 4u * b);
+			e = q[0] == key[0] && q[1] == key[1] && (nk < 3u || q[2] == key[2]);
+			v = nk < 3u ? q[2] : q[3];
+		} else {
+			const u32x4 q = ld4(H, tbl + 8u * b), r = ld4(H, tbl + 8u * b + 4u);
+			e = q[0] == key[0] && q[1] == key[1] && q[2] == key[2] && q[3] == key[3];
+			v = r[0];
+		}
 		val = (act && e && v != 0u) ? v : val;
 	}
 	return val;
+}
+
+// the class record's own table
+template <typename D, typename T>
+__device__ __forceinline__ uint32_t bv_lookup(const D &cr, T H, const uint32_t key[4], bool act)
+{
+	return bv_probe(H, key, act, cr(1), cr(9), cr(10), cr(11), cr(12));
 }
 
 // Classification block evaluation of one CoS for the lanes in `act`
@@ -1280,18 +1310,20 @@ __device__ __forceinline__ void bv_eval(const D &blk, T H, bool act, const Pkt &
 					const Fields &x, uint32_t &hit, uint32_t &nxt, uint32_t &nmark,
 					uint32_t &nleaf)
 {
-	const auto hb = blk.vec(0);   // the block header (words 0-7)
+	const auto hb = blk.hdr();   // the block header (words 0-7)
 	const uint32_t mode = FM >= 0 ? (uint32_t)FM : hb(0), ncls = hb(1), res = hb(2);
 	uint32_t first = BV_NONE;
 	if (mode == 0u) {
 		// direct: one class, the slot holds the result word of the first
 		// live rule of its key (BV_EMPTY: none); a miss takes the block's
-		// "no term" rule (0: none)
-		const auto cr = blk.vec(8u);
+		// "no term" rule (0: none).  The class record is shared by the
+		// direct blocks with the same class (header word 2); the header
+		// holds the miss word and the table (bucket count, offset, m1, m2)
+		const auto cr = blk.root(hb(2));
 		uint32_t key[4];
 		const bool present = bv_key(cr, k, p, x, key);
-		const uint32_t val = bv_lookup(cr, H, key, act && present);
-		const uint32_t rw = val != 0u ? (val == BV_EMPTY ? 0u : val) : cr(2);
+		const uint32_t val = bv_probe(H, key, act && present, cr(1), hb(4), hb(5), hb(6), hb(7));
+		const uint32_t rw = val != 0u ? (val == BV_EMPTY ? 0u : val) : hb(3);
 		const bool h = act && rw != 0u;
 		nxt = h ? (rw & 0xffu) : nxt;
 		nleaf = h ? ((rw >> 8) & 1u) : nleaf;
@@ -1634,9 +1666,8 @@ __device__ __forceinline__ void store_window(uint32_t *W, uint32_t lane, const u
 // read as zero already): bytes b..3 of the partial dword with one byte store
 // (b odd) and one 16-bit store (b <= 2) -- stores that are not needed go to
 // the lane's pad dword, which is zero anyway -- then the next three whole
-// dwords without a test: rows past the piece are zero (pieces past the
-// frame, or the zero rows WIN/4 .. WIN/4+2 where a frame of >= WIN bytes
-// starts).
+// dwords (clamped to the zero row WIN/4): rows past the piece are zero
+// (pieces past the frame, or the zero row).
 __device__ __forceinline__ void zero_tail(uint32_t *W, uint32_t lane, uint32_t len)
 {
 	const uint32_t pad = (WIN / 4) * RS + lane;
@@ -1646,10 +1677,10 @@ __device__ __forceinline__ void zero_tail(uint32_t *W, uint32_t lane, uint32_t l
 	const uint32_t pb = (dw * RS + lane) * 4u;
 	W8[(part && (b & 1u)) ? pb + b : pad * 4u + 1u] = 0;
 	*(uint16_t *)(W8 + ((part && b <= 2u) ? pb + 2u : pad * 4u + 2u)) = 0;
-	uint32_t *z = W + min((len + 3u) >> 2, (uint32_t)(WIN / 4)) * RS + lane;
-	z[0] = 0u;
-	z[RS] = 0u;
-	z[2 * RS] = 0u;
+	const uint32_t r0 = (len + 3u) >> 2;
+	W[min(r0, (uint32_t)(WIN / 4)) * RS + lane] = 0u;
+	W[min(r0 + 1u, (uint32_t)(WIN / 4)) * RS + lane] = 0u;
+	W[min(r0 + 2u, (uint32_t)(WIN / 4)) * RS + lane] = 0u;
 }
 
 // Make this wave's LDS writes visible to its own later LDS reads by other
@@ -1973,10 +2004,10 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 			uint32_t hit = 0, nleaf = 0, nxt = 0, nmark = 0;
 			const bool g = pend != 0u;
 			if constexpr (FM >= 0) {
-				bv_eval<FM>(DescU{ hc + d_bv }, H, g, k, p, x, hit, nxt, nmark, nleaf);
+				bv_eval<FM>(DescU{ hc + d_bv, hc }, H, g, k, p, x, hit, nxt, nmark, nleaf);
 			} else {
 				if (d_bv != 0u && d_nr != 0u)
-					bv_eval(DescU{ hc + d_bv }, H, g, k, p, x, hit, nxt, nmark, nleaf);
+					bv_eval(DescU{ hc + d_bv, hc }, H, g, k, p, x, hit, nxt, nmark, nleaf);
 				else
 					linear_scan(prog, d_rec0, d_nr, g, k, p, x, hit, nxt, nmark);
 			}
@@ -2012,7 +2043,7 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 				const cword_t ce = hc + COS_WORDS * (uint32_t)c1;
 				const uint32_t nr = ce[C_NR], bv = ce[C_BV];
 				if (bv != 0u && nr != 0u)
-					bv_eval(DescU{ hc + bv }, H, g, k, p, x, hit, nxt, nmark, nleaf);
+					bv_eval(DescU{ hc + bv, hc }, H, g, k, p, x, hit, nxt, nmark, nleaf);
 				else
 					linear_scan(prog, ce[C_REC0], nr, g, k, p, x, hit, nxt, nmark);
 			}
