@@ -175,9 +175,12 @@ int mi_cls_rules_load(mi_cls_ctx_t *ctx, const void *tbl, size_t bytes, void *st
 
 /* Parse + classify n packets.
  *   pkts_dev  packed packet bytes; each packet starts at pkts_dev + off_dev[i]
- *             (16-byte aligned offsets take the fast staging path; others are
- *             still correct) and the buffer must be readable up to the next
- *             16-byte boundary after each packet (true of any hipMalloc).
+ *             (any alignment).  Loads are 16-B pieces at frame-relative
+ *             offsets, so the buffer must be readable up to
+ *             off_dev[i] + round_up(len_dev[i], 16) for every packet: when
+ *             off_dev[i] is not a multiple of 16 that is up to 15 bytes past
+ *             the next 16-byte boundary after the packet (a batch whose
+ *             allocation ends right after its last frame needs 16 B of slack).
  *   off_dev   uint32 byte offsets, len_dev uint16 frame lengths (FCS stripped)
  *   out_dev   n result records
  * Stream-ordered on `stream`; returns after the launch is enqueued. */
