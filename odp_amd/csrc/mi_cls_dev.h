@@ -1402,47 +1402,73 @@ __device__ __forceinline__ void bv_eval(const D &blk, T H, bool act, const Pkt &
 				}
 			}
 		}
+		// the lane's candidates (1 + rule), compacted: a packet has at most
+		// one per primary class, and usually far fewer than the block has
+		// primary classes (config4: two of four), so two checks run always
+		// and the others only if some lane needs them.  The smallest holding
+		// candidate wins, so the order does not matter.
+		uint32_t cl[BV_MAX_CLS];
+#pragma unroll
+		for (uint32_t i = 0; i < BV_MAX_CLS; ++i)
+			cl[i] = 0u;
+		uint32_t nc = 0;
 #pragma unroll
 		for (uint32_t kc = 0; kc < BV_MAX_CLS; ++kc) {
 			if (kc < ncls && ((pm >> kc) & 1u)) {
 				const uint32_t c1 = cand[kc];
-				const bool tr = act && c1 != 0u && c1 - 1u < first;
-				if (__ballot(tr) != 0ull) {
-					const uint32_t ra = rec0 + (tr ? c1 - 1u : 0u) * rw;
-					const u32x4 q0 = ld4(H, ra);
-					u32x4 q1 = { 0u, 0u, 0u, 0u }, q2 = { 0u, 0u, 0u, 0u };
-					if (rw > 4u)
-						q1 = ld4(H, ra + 4u);
-					if (rw > 8u)
-						q2 = ld4(H, ra + 8u);
-					const uint32_t tm = q0[0];
-					bool ok = (tm >> 31) == 0u;
-					if (rw == 4u && ncls > 3u) {
-						// compact record: the constrained classes' values
-						// in class order
 #pragma unroll
-						for (uint32_t c2 = 0; c2 < BV_MAX_CLS; ++c2) {
-							if (c2 < ncls) {
-								const uint32_t j = (uint32_t)__builtin_popcount(tm & ((1u << c2) - 1u));
-								const uint32_t w = j == 0u ? q0[1] : (j == 1u ? q0[2] : q0[3]);
-								const bool need = (tm >> c2) & 1u;
-								ok = ok && (!need || (((prm >> c2) & 1u) && cmpv[c2] == w));
-							}
-						}
-					} else {
-#pragma unroll
-						for (uint32_t c2 = 0; c2 < BV_MAX_CLS; ++c2) {
-							if (c2 < ncls) {
-								const uint32_t w = c2 < 3u ? q0[1 + c2] : (c2 < 7u ? q1[c2 - 3u] : q2[0]);
-								const bool need = (tm >> c2) & 1u;
-								ok = ok && (!need || (((prm >> c2) & 1u) && cmpv[c2] == w));
-							}
-						}
-					}
-					first = (tr && ok) ? c1 - 1u : first;
-				}
+				for (uint32_t i = 0; i <= kc; ++i)
+					cl[i] = (c1 != 0u && nc == i) ? c1 : cl[i];
+				nc += c1 != 0u ? 1u : 0u;
 			}
 		}
+		const bool compact = rw == 4u && ncls > 3u;
+		auto check = [&](uint32_t c1) {
+			const bool tr = act && c1 != 0u && c1 - 1u < first;
+			if (__ballot(tr) == 0ull)
+				return;
+			const uint32_t ra = rec0 + (tr ? c1 - 1u : 0u) * rw;
+			const u32x4 q0 = ld4(H, ra);
+			const uint32_t tm = q0[0];
+			bool ok = (tm >> 31) == 0u;
+			if (compact) {
+				// compact record: the values of the <= 3 constrained
+				// classes in class order; the packet's value of the
+				// j-th one is picked by select (no per-class branches)
+				uint32_t t = tm & 0xffu;
+#pragma unroll
+				for (uint32_t j = 0; j < 3; ++j) {
+					const uint32_t c = (uint32_t)__builtin_ctz(t | 0x100u);
+					t &= t - 1u;
+					uint32_t pv = 0u;
+#pragma unroll
+					for (uint32_t i = 0; i < BV_MAX_CLS; ++i)
+						pv = c == i ? cmpv[i] : pv;
+					ok = ok && (c >= BV_MAX_CLS || (((prm >> c) & 1u) && pv == q0[1 + j]));
+				}
+			} else {
+				u32x4 q1 = { 0u, 0u, 0u, 0u }, q2 = { 0u, 0u, 0u, 0u };
+				if (rw > 4u)
+					q1 = ld4(H, ra + 4u);
+				if (rw > 8u)
+					q2 = ld4(H, ra + 8u);
+#pragma unroll
+				for (uint32_t c2 = 0; c2 < BV_MAX_CLS; ++c2) {
+					if (c2 < ncls) {
+						const uint32_t w = c2 < 3u ? q0[1 + c2] : (c2 < 7u ? q1[c2 - 3u] : q2[0]);
+						const bool need = (tm >> c2) & 1u;
+						ok = ok && (!need || (((prm >> c2) & 1u) && cmpv[c2] == w));
+					}
+				}
+			}
+			first = (tr && ok) ? c1 - 1u : first;
+		};
+		check(cl[0]);
+		check(cl[1]);
+#pragma unroll
+		for (uint32_t i = 2; i < BV_MAX_CLS; ++i)
+			if (__ballot(cl[i] != 0u) != 0ull)
+				check(cl[i]);
 	} else {
 		// candidate: key id per class, then the candidates' records
 		const uint32_t rec0 = hb(4), rw = hb(5);
