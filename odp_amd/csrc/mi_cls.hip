@@ -400,7 +400,8 @@ static Key4 class_value(const mi_term_t &t, const ClassKey &ck)
 //    with no classified term (it matches everything); a candidate holds iff
 //    its record's key ids equal the packet's, and the smallest one wins.
 static bool build_bv(const mi_cos_t *cs, const mi_rule_t *rs, const mi_term_t *ts, uint32_t nrules,
-		     uint32_t base, std::vector<uint32_t> &blk, std::array<uint32_t, 16> &shared)
+		     uint32_t base, std::vector<uint32_t> &blk,
+		     std::vector<std::pair<uint32_t, std::array<uint32_t, 16>>> &shared)
 {
 	std::map<ClassKey, uint32_t> cls;
 	std::vector<ClassKey> cls_list;
@@ -497,12 +498,16 @@ static bool build_bv(const mi_cos_t *cs, const mi_rule_t *rs, const mi_term_t *t
 		if (alive[r] && tmask[r] == 0u)
 			wc_first = r;
 	// header (8) | classes (16 each) | results | [records] | per class: table [, lists].
-	// Direct blocks: header (8: mode, 1, shared class record, miss result,
-	// bucket count, table, m1, m2) | table; their 16-word class record
-	// (`shared`, the block-specific words zero) is stored once per distinct
-	// record in the hot region by assemble(), which patches word 2
+	// Split class (direct blocks): the 16-word class record holds only what
+	// the class is (kind, key words, masks, field descriptor); it is stored
+	// once per distinct record in the hot region by assemble(), which
+	// patches its index into the block's 6-word class info in header words
+	// 2-7 (shared record, miss word, bucket count, table, m1, m2); the block
+	// is header | table.  (Splitting the bitmap blocks' classes the same way
+	// measured slower on config5: the per-lane rounds read more words.)
+	const bool split = mode == 0u;
 	blk.assign(mode == 0u ? 8u : 8u + BV_CLS_WORDS * ncls, 0);
-	shared.fill(0u);
+	shared.clear();
 	blk[0] = mode;
 	blk[1] = ncls;
 	blk[3] = wc_first;
@@ -662,9 +667,12 @@ static bool build_bv(const mi_cos_t *cs, const mi_rule_t *rs, const mi_term_t *t
 		if (!cuckoo_place(keys, ck.nkey, bsz, nb, m1, m2, slot_of))
 			return false;
 		const uint32_t cbase = 8 + BV_CLS_WORDS * c;
+		const uint32_t ib = mode == 0u ? 2u : 8u + 8u * c;   // split class info
+		std::array<uint32_t, 16> rec;
+		rec.fill(0u);
 		auto setc = [&](uint32_t w, uint32_t v) {
-			if (mode == 0u)
-				shared[w] = v;
+			if (split)
+				rec[w] = v;
 			else
 				blk[cbase + w] = v;
 		};
@@ -676,18 +684,18 @@ static bool build_bv(const mi_cos_t *cs, const mi_rule_t *rs, const mi_term_t *t
 		const uint32_t fl0 = mode == 0u ? first_live(c, nullptr) : 0u;
 		const uint32_t miss = mode == 0u ? (fl0 == BV_NONE ? 0u : res_word(fl0) | BV_RES_VALID)
 			: (mode == 2u ? row_of(c, nullptr) : (mode == 3u ? base + rows_at + 4u * miss_id[c] : 0u));
-		if (mode == 0u)
-			blk[3] = miss;
+		if (split)
+			blk[ib + 1] = miss;
 		else
 			blk[cbase + 2] = miss;
 		setc(3, ck.offset);
 		setc(4, ck.size);
 		for (int i = 0; i < 4; ++i)
 			setc(5 + i, ck.mask[i]);
-		if (mode == 0u) {
-			blk[4] = nb;
-			blk[6] = m1;
-			blk[7] = m2;
+		if (split) {
+			blk[ib + 2] = nb;
+			blk[ib + 4] = m1;
+			blk[ib + 5] = m2;
 		} else {
 			blk[cbase + 9] = nb;
 			blk[cbase + 11] = m1;
@@ -710,10 +718,12 @@ static bool build_bv(const mi_cos_t *cs, const mi_rule_t *rs, const mi_term_t *t
 			setc(BVC_AO, d.add | (d.alt << 16));
 			setc(BVC_DESC, (gate & 0xffffffu) | (d.base << 24) | (ac << 26) | (fl << 28));
 		}
+		if (split)
+			shared.emplace_back(ib, rec);
 		align4();   // 16-B buckets / slots
 		const uint32_t tbl_off = (uint32_t)blk.size();
-		if (mode == 0u)
-			blk[5] = base + tbl_off;
+		if (split)
+			blk[ib + 3] = base + tbl_off;
 		else
 			blk[cbase + 10] = base + tbl_off;
 		// empty slots keep key words 0 and value 0: a miss (every stored
@@ -782,20 +792,20 @@ static int assemble(const void *tbl, uint32_t **out, size_t *out_words)
 	}
 	if (!getenv("MI_CLS_NO_BV")) {
 		// direct blocks' class records, one copy per distinct record
-		std::map<std::array<uint32_t, 16>, std::vector<uint32_t>> shared_users;
+		std::map<std::array<uint32_t, 16>, std::vector<uint32_t>> shared_users;   // -> patch words
 		for (uint32_t s = 0; s < h->num_cos; ++s) {
 			if (!cs[s].valid || cs[s].num_rules == 0)
 				continue;
 			std::vector<uint32_t> blk;
-			std::array<uint32_t, 16> shared;
+			std::vector<std::pair<uint32_t, std::array<uint32_t, 16>>> shared;
 			while (hot.size() & 3u)   // blocks start 16-B aligned (16-B row / bucket reads)
 				hot.push_back(0);
 			const uint32_t base = (uint32_t)hot.size();
 			if (build_bv(cs, rs + cs[s].rule_begin, ts, cs[s].num_rules, base, blk, shared)) {
 				hot[COS_WORDS * s + C_BV] = base;
 				hot.insert(hot.end(), blk.begin(), blk.end());
-				if (blk[0] == 0u)
-					shared_users[shared].push_back(base);
+				for (auto &sh : shared)
+					shared_users[sh.second].push_back(base + sh.first);
 			}
 		}
 		for (auto &kv : shared_users) {
@@ -803,8 +813,8 @@ static int assemble(const void *tbl, uint32_t **out, size_t *out_words)
 				hot.push_back(0);
 			const uint32_t at = (uint32_t)hot.size();
 			hot.insert(hot.end(), kv.first.begin(), kv.first.end());
-			for (uint32_t b : kv.second)
-				hot[b + 2] = at;
+			for (uint32_t w : kv.second)
+				hot[w] = at;
 		}
 	}
 	// cold region: 16-word rule records (+ ext terms appended after them)

@@ -1076,27 +1076,39 @@ enum { DH_MAGIC = 0, DH_NCOS, DH_DEFAULT, DH_ERROR, DH_DEFAULT_VALID, DH_USED, D
 // when its rules fall into at most BV_MAX_CLS key classes (a key class is one
 // (term kind, mask[, offset, size]) combination).  build_bv() explains the
 // modes; the layout (word indices into the hot region) is:
-//   b[0] mode (0 direct, 1 candidate, 2 bitmap, 3 wide bitmap), b[1] #classes,
-//   b[2] result words (dst | leaf<<8 | mark<<16 per rule; leaf = the
-//   destination CoS has no rules, so the descent ends there), b[3] first rule
-//   without a classified term (BV_NONE: none), b[4] rule records (bitmap:
-//   alive row; wide: block-relative index of the nw-word alive row), b[5]
-//   record words, b[6] wide: nw = words per row
-//   b[8 + 16 k ...] class k: kind, nkey, miss value (direct: first rule,
-//                   bitmap: row, wide: index of the miss row), offset, size,
-//                   mask[4], #slots, table offset, cuckoo multipliers m1, m2,
-//                   list base
-//   table slot (nkey + 1 words): key words, value (0: empty)
-//     direct: 1 + first live rule with this key or without a term of the
-//             class (BV_EMPTY: none)
+//   b[0] mode (0 direct, 1 candidate, 2 bitmap, 3 wide bitmap, 4 single
+//   candidate), b[1] #classes, b[2] result words (dst | leaf<<8 | mark<<16
+//   per rule; leaf = the destination CoS has no rules, so the descent ends
+//   there), b[3] first rule without a classified term (BV_NONE: none), b[4]
+//   rule records (bitmap: alive row; wide: block-relative index of the
+//   nw-word alive row), b[5] record words, b[6] wide: nw = words per row
+//   class record (16 words): kind, nkey, miss value (wide: index of the miss
+//                   row), offset (custom) / tag bit (merged ports), size,
+//                   mask[4], #buckets, table offset, cuckoo multipliers m1,
+//                   m2, list base, field descriptor (BVC_AO, BVC_DESC)
+//   modes 1-4: class k's record at b[8 + 16 k]
+//   direct blocks (mode 0, split class): the record holds only what the
+//                   class is and is shared by every direct block with that
+//                   class; the block keeps the 6-word class info in b[2..7]:
+//                   shared record index, miss word, #buckets, table offset,
+//                   m1, m2 (no results array)
+//   table (16-B aligned): one-word keys 2 slots of (key, value) per 16-B
+//             bucket; 2-3-word keys one 16-B slot (key words, value);
+//             4-word keys one 32-B slot; value 0: empty
+//     direct: the result word of the first live rule with this key or
+//             without a term of the class, | BV_RES_VALID (BV_EMPTY: none)
 //     bitmap: the 32-bit row of rules with this key or without a term
 //     wide:   index of the nw-word row of rules with this key or without a
 //             term of the class (rows are deduplicated)
 //     candidate: key id | list length << 12 | list offset << 20; the list
 //             holds the rules filed under this key, in scan order
+//     single candidate: key id << 16 | 1 + the rule filed under the key
 //   rule record (candidate, 1 + ceil(#classes / 2) words): constrained-
 //             class mask (bit 31: never holds), then the required key id of
 //             class c in half c & 1 of word 1 + c / 2
+//   rule record (single candidate, 4 or 8 words): constrained-class mask,
+//             then the required value (key id for longer keys) per class,
+//             or (compact, 4 words) of the <= 3 constrained classes in order
 
 __device__ __forceinline__ bool eq1(uint32_t x, uint32_t m, uint32_t v)
 {
@@ -1162,6 +1174,7 @@ struct DescV {
 struct DescU {
 	cword_t p;
 	cword_t h;              // start of the hot region (root())
+	static constexpr bool per_lane = false;
 	__device__ __forceinline__ uint32_t operator()(uint32_t i) const { return p[i]; }
 	__device__ __forceinline__ DescU at(uint32_t o) const { return DescU{ p + o, h }; }
 	// 16 words at o, loaded at once
@@ -1170,6 +1183,7 @@ struct DescU {
 		return DescV{ *(const __attribute__((address_space(4))) u32x16 *)(p + o) };
 	}
 	__device__ __forceinline__ DescV hdr() const { return vec(0u); }
+	__device__ __forceinline__ DescV vec8(uint32_t o) const { return vec(o); }
 	// 16 words at hot-region word o (a direct block's shared class record)
 	__device__ __forceinline__ DescV root(uint32_t o) const { return DescU{ h + o, h }.vec(0u); }
 };
@@ -1190,8 +1204,10 @@ __device__ __forceinline__ u32x4 ld4(gword_t H, uint32_t i)
 template <typename T> struct DescL {
 	T p;
 	uint32_t b;
+	cword_t h;              // the hot region in the constant address space (scalar loads)
+	static constexpr bool per_lane = true;
 	__device__ __forceinline__ uint32_t operator()(uint32_t i) const { return p[b + i]; }
-	__device__ __forceinline__ DescL at(uint32_t o) const { return DescL{ p, b + o }; }
+	__device__ __forceinline__ DescL at(uint32_t o) const { return DescL{ p, b + o, h }; }
 	__device__ __forceinline__ DescV vec(uint32_t o) const
 	{
 		const u32x4 q0 = ld4(p, b + o), q1 = ld4(p, b + o + 4u), q2 = ld4(p, b + o + 8u),
@@ -1201,16 +1217,17 @@ template <typename T> struct DescL {
 			      q2[0], q2[1], q2[2], q2[3], q3[0], q3[1], q3[2], q3[3] };
 		return d;
 	}
-	__device__ __forceinline__ DescV root(uint32_t o) const { return DescL{ p, o }.vec(0u); }
-	// the 8-word block header
-	__device__ __forceinline__ DescV hdr() const
+	__device__ __forceinline__ DescV root(uint32_t o) const { return DescL{ p, o, h }.vec(0u); }
+	// 8 words at o (the block header, a split class's info)
+	__device__ __forceinline__ DescV vec8(uint32_t o) const
 	{
-		const u32x4 q0 = ld4(p, b), q1 = ld4(p, b + 4u);
+		const u32x4 q0 = ld4(p, b + o), q1 = ld4(p, b + o + 4u);
 		DescV d;
 		d.v = u32x16{ q0[0], q0[1], q0[2], q0[3], q1[0], q1[1], q1[2], q1[3],
 			      0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u };
 		return d;
 	}
+	__device__ __forceinline__ DescV hdr() const { return vec8(0u); }
 };
 
 // Key of a packet for one class: the masked field the class's terms
@@ -1298,6 +1315,29 @@ __device__ __forceinline__ uint32_t bv_lookup(const D &cr, T H, const uint32_t k
 	return bv_probe(H, key, act, cr(1), cr(9), cr(10), cr(11), cr(12));
 }
 
+// Key of a packet for a split class (direct and bitmap blocks: the class
+// record is shared, at hot-region word `ro`).  Per-lane blocks whose lanes all
+// use one record (a tree level of same-class CoS) read it once with scalar
+// loads and decode it in SGPRs.  Returns the presence; nk = key words.
+template <typename D>
+__device__ __forceinline__ bool split_key(const D &blk, uint32_t ro, bool act, const Pkt &k,
+					  const Parsed &p, const Fields &x, uint32_t key[4], uint32_t &nk)
+{
+	if constexpr (D::per_lane) {
+		const unsigned long long am = __ballot(act);
+		const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane(
+			(int)ro, am ? (int)__builtin_ctzll(am) : 0);
+		if (__ballot(act && ro != r0) == 0ull) {
+			const auto cu = DescU{ blk.h + r0, blk.h }.vec(0u);
+			nk = cu(1);
+			return bv_key(cu, k, p, x, key);
+		}
+	}
+	const auto cr = blk.root(ro);
+	nk = cr(1);
+	return bv_key(cr, k, p, x, key);
+}
+
 // Classification block evaluation of one CoS for the lanes in `act`
 // (see build_bv for the two modes).  `blk` reads the CoS's block (wave-
 // uniform or per lane); H is the hot region the block's offsets index.  On
@@ -1319,10 +1359,9 @@ __device__ __forceinline__ void bv_eval(const D &blk, T H, bool act, const Pkt &
 		// "no term" rule (0: none).  The class record is shared by the
 		// direct blocks with the same class (header word 2); the header
 		// holds the miss word and the table (bucket count, offset, m1, m2)
-		const auto cr = blk.root(hb(2));
-		uint32_t key[4];
-		const bool present = bv_key(cr, k, p, x, key);
-		const uint32_t val = bv_probe(H, key, act && present, cr(1), hb(4), hb(5), hb(6), hb(7));
+		uint32_t key[4], nk;
+		const bool present = split_key(blk, hb(2), act, k, p, x, key, nk);
+		const uint32_t val = bv_probe(H, key, act && present, nk, hb(4), hb(5), hb(6), hb(7));
 		const uint32_t rw = val != 0u ? (val == BV_EMPTY ? 0u : val) : hb(3);
 		const bool h = act && rw != 0u;
 		nxt = h ? (rw & 0xffu) : nxt;
@@ -2054,7 +2093,7 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 					const bool empty = pend != 0u && my_nr == 0u;
 					const bool bvl = pend != 0u && my_nr != 0u && my_bv != 0u;
 					if (__ballot(bvl))
-						bv_eval(DescL<hot_t>{ H, my_bv }, H, bvl, k, p, x, hit, nxt, nmark,
+						bv_eval(DescL<hot_t>{ H, my_bv, hc }, H, bvl, k, p, x, hit, nxt, nmark,
 							nleaf);
 					handled = (bvl || empty) ? 1u : 0u;
 					act = pend != 0u && handled == 0u;
