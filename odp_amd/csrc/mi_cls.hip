@@ -1086,7 +1086,7 @@ extern "C" int mi_cls_classify(mi_cls_ctx_t *c, const uint8_t *pkts, const uint3
 	const size_t hot_bytes = (((size_t)c->hot_words + 3u) & ~(size_t)3u) * sizeof(uint32_t);
 	// static LDS of a block: windows, stats histogram, L4 table (+ the
 	// CRC-32C tables of the pktin-option kernels)
-	const size_t st_ck = c->opt != 0 ? 1024 : 0;
+	const size_t st_ck = c->opt != 0 ? 1024 + CRC_ZN + 64 : 0;
 	auto st_of = [st_ck](int w) {
 		return sizeof(uint32_t) * ((size_t)w * RS * WROWS + MAX_STATS_COS + 256 + st_ck);
 	};

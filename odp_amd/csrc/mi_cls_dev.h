@@ -415,9 +415,16 @@ __device__ __forceinline__ Parsed parse_packet(const Pkt &k, uint32_t opt)
 // caller-supplied init, no final inversion), as slicing-by-4 tables: t[0] is
 // the byte table, t[k][i] = t[k-1][i] >> 8 ^ t[0][t[k-1][i] & 0xff], so four
 // bytes advance with four independent lookups instead of four dependent ones.
+// z[m] = x^(512 m) and y[r] = x^(8 r) mod P in the reflected domain (the
+// register that m 64-byte / r one-byte zero blocks turn 0x80000000 = x^0
+// into): the shifts that combine CRCs of separately processed pieces
+// (sctp_crc_wave; zlib's crc32_combine arithmetic).
+#define CRC_ZN 256          // pieces of 64 B a frame may have on the cooperative path
 struct Crc32cTab {
 	uint32_t t[4][256];
-	constexpr Crc32cTab() : t()
+	uint32_t z[CRC_ZN];
+	uint32_t y[64];
+	constexpr Crc32cTab() : t(), z(), y()
 	{
 		for (uint32_t i = 0; i < 256; ++i) {
 			uint32_t c = i;
@@ -428,6 +435,18 @@ struct Crc32cTab {
 		for (int k = 1; k < 4; ++k)
 			for (uint32_t i = 0; i < 256; ++i)
 				t[k][i] = (t[k - 1][i] >> 8) ^ t[0][t[k - 1][i] & 0xffu];
+		uint32_t r = 0x80000000u;
+		for (uint32_t i = 0; i < 64; ++i) {
+			y[i] = r;
+			r = t[0][r & 0xffu] ^ (r >> 8);
+		}
+		r = 0x80000000u;
+		for (uint32_t m = 0; m < CRC_ZN; ++m) {
+			z[m] = r;
+			for (int i = 0; i < 16; ++i)   // 64 zero bytes, four at a time
+				r = t[3][r & 0xffu] ^ t[2][(r >> 8) & 0xffu] ^ t[1][(r >> 16) & 0xffu] ^
+				    t[0][r >> 24];
+		}
 	}
 };
 static __constant__ Crc32cTab c_crc32c;
@@ -600,6 +619,106 @@ __device__ __forceinline__ uint32_t sctp_crc(const Pkt &k, __amdgpu_buffer_rsrc_
 	return ~crc;
 }
 
+// a * b mod P in the reflected domain (zlib multmodp), branch-free
+__device__ __forceinline__ uint32_t crc_mulmod(uint32_t a, uint32_t b)
+{
+	uint32_t p = 0;
+#pragma unroll
+	for (int i = 31; i >= 0; --i) {
+		p ^= ((a >> i) & 1u) ? b : 0u;
+		b = (b >> 1) ^ ((b & 1u) ? 0x82F63B78u : 0u);
+	}
+	return p;
+}
+
+__device__ __forceinline__ uint32_t wave_scan_xor(uint32_t v, uint32_t lane)
+{
+	v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);
+	v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);
+	v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);
+	v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);
+	const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)v, 15);
+	const uint32_t r1 = (uint32_t)__builtin_amdgcn_readlane((int)v, 31);
+	const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)v, 47);
+	const uint32_t row = lane >> 4;
+	return v ^ (row >= 1u ? r0 : 0u) ^ (row >= 2u ? r1 : 0u) ^ (row >= 3u ? r2 : 0u);
+}
+
+// Wave-cooperative CRC-32C of the SCTP check (all 64 lanes active): lane f
+// asks for the CRC over frame bytes [l4, len) of its frame (batch offset
+// boff) with the checksum field [l4 + 8, l4 + 12) taken as zero, init ~0,
+// inverted -- `cnt` = ceil((len - l4) / 64) pieces of 64 B counted from the
+// END of the frame (piece m = [len - 64 (m+1), len - 64 m)), dealt out 64 per
+// round as in ck_sum_wave.  CRC is linear over GF(2): a lane computes the
+// raw CRC (init 0) of its piece, bytes below l4 and the checksum field as
+// zero -- leading zeros leave a zero register unchanged, and pieces aligned
+// to the end have no trailing partial block -- and shifts it by the 64 m
+// bytes after it (x^(512 m), table z); the frame's register is the XOR of
+// its pieces' (prefix XOR over the round), plus the init's contribution
+// ~0 * x^(8 (len - l4)).  Returns the finished CRC for the asking lanes.
+__device__ __forceinline__ uint32_t sctp_crc_wave(__amdgpu_buffer_rsrc_t rs, uint32_t boff,
+						  uint32_t l4, uint32_t len, uint32_t cnt,
+						  uint32_t lane, const uint32_t *tab)
+{
+	const uint32_t *zt = tab + 1024u, *yt = zt + CRC_ZN;
+	const uint32_t incl = wave_scan_add(cnt, lane);
+	const uint32_t first = incl - cnt;
+	const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, WAVE - 1);
+	const uint32_t geo = l4 | (len << 16);
+	uint32_t acc = 0;
+	for (uint32_t B = 0; B < total; B += WAVE) {
+		const uint32_t g = B + lane;
+		uint32_t lo = 0;
+#pragma unroll
+		for (uint32_t st = WAVE / 2; st >= 1; st >>= 1) {
+			const uint32_t c = lo + st;
+			lo = lane_get(first, c) <= g ? c : lo;
+		}
+		const uint32_t m = g - lane_get(first, lo);   // piece number from the end
+		const uint32_t gg = lane_get(geo, lo);
+		const uint32_t ob = lane_get(boff, lo);
+		const bool live = g < total;
+		const int32_t fl4 = (int32_t)(gg & 0xffffu), flen = (int32_t)(gg >> 16);
+		const int32_t start = flen - 64 * (int32_t)(m + 1u);   // frame-relative
+		u32x4 v[4];
+#pragma unroll
+		for (int32_t i = 0; i < 4; ++i) {
+			// 16-B pieces wholly below l4 are not needed; pieces starting
+			// before the batch read as zero (OOB offset), bytes below l4
+			// are masked anyway
+			const int32_t o = start + 16 * i;
+			const bool need = live && o + 16 > fl4;
+			v[i] = __builtin_amdgcn_raw_buffer_load_b128(
+				rs, (need && (int32_t)ob + o >= 0) ? (uint32_t)((int32_t)ob + o) : OOB_OFF, 0, 0);
+		}
+		uint32_t crc = 0;
+		const int32_t rel = fl4 - start;   // l4 relative to the piece start
+#pragma unroll
+		for (int32_t d = 0; d < 16; ++d) {
+			const int32_t a = rel - 4 * d;         // l4 relative to this dword
+			// keep bytes >= l4, drop the checksum field [l4 + 8, l4 + 12)
+			const uint32_t lo_cut = (uint32_t)min(max(a, 0), 4);
+			const uint32_t f0 = (uint32_t)min(max(a + 8, 0), 4), f1 = (uint32_t)min(max(a + 12, 0), 4);
+			const uint64_t ones = 0xFFFFFFFFull;
+			const uint32_t keep = (uint32_t)(ones << (8u * lo_cut)) &
+					      ~((uint32_t)(ones << (8u * f0)) & ~(uint32_t)(ones << (8u * f1)));
+			crc = crc32c_u32(tab, crc, v[d >> 2][d & 3] & keep);
+		}
+		// shift by the 64 m bytes after the piece
+		const uint32_t r = live ? crc_mulmod(crc, zt[min(m, (uint32_t)CRC_ZN - 1u)]) : 0u;
+		const uint32_t P = wave_scan_xor(r, lane);
+		const uint32_t a0 = first > B ? first - B : 0u;
+		const uint32_t e = min(incl > B ? incl - B : 0u, (uint32_t)WAVE);
+		const uint32_t pe = lane_get(P, e > 0u ? e - 1u : 0u);
+		const uint32_t pa = lane_get(P, a0 > 0u ? a0 - 1u : 0u);
+		acc ^= (e > a0) ? (pe ^ (a0 > 0u ? pa : 0u)) : 0u;
+	}
+	// the init register ~0 shifted over the whole message
+	const uint32_t n = len - l4;
+	const uint32_t sh = crc_mulmod(zt[min(n >> 6, (uint32_t)CRC_ZN - 1u)], yt[n & 63u]);
+	return ~(acc ^ crc_mulmod(0xFFFFFFFFu, sh));
+}
+
 // _odp_packet_l4_chksum (odp_packet.c:2065-2138) for the lanes whose parse
 // returned 0, with the partial sums parse_ipv4 / parse_ipv6 / parse_tcp /
 // parse_udp / parse_sctp prepare (odp_parse.c:146-148, 212-214, 267-275,
@@ -644,8 +763,17 @@ __device__ __forceinline__ void l4_chksum(const Pkt &k, Parsed &p, uint32_t opt,
 	}
 	bool bad = sum && ck_finalize(s) != 0xffffu;   // ~sum != 0
 	if (__ballot(kind == 3u) != 0ull) {
-		if (kind == 3u)
-			bad = sctp_crc(k, rs, boff, l4, crc_tab) != r32(k, l4 + 8u);
+		// frames with at most CRC_ZN 64-B pieces: the wave cooperates;
+		// longer (jumbo) ones: one lane walks its frame
+		const bool wv = kind == 3u && len - l4 < 64u * CRC_ZN;
+		const uint32_t crc = sctp_crc_wave(rs, boff, l4, len, wv ? (len - l4 + 63u) >> 6 : 0u,
+						   lane, crc_tab);
+		if (wv)
+			bad = crc != r32(k, l4 + 8u);
+		if (__ballot(kind == 3u && !wv) != 0ull) {
+			if (kind == 3u && !wv)
+				bad = sctp_crc(k, rs, boff, l4, crc_tab) != r32(k, l4 + 8u);
+		}
 	}
 	if (kind != 0u) {
 		p.flags |= F_L4CK_DONE;
@@ -1813,7 +1941,8 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 	__shared__ uint32_t s_win[NW * RS * WROWS];
 	__shared__ uint32_t s_cnt[MAX_STATS_COS];
 	__shared__ uint32_t s_l4[256];
-	__shared__ uint32_t s_crc[CK ? 1024 : 1];   // CRC-32C slicing tables (pktin options)
+	// CRC-32C slicing tables and piece shifts (pktin options)
+	__shared__ uint32_t s_crc[CK ? 1024 + CRC_ZN + 64 : 1];
 
 	const uint32_t lane = threadIdx.x & (WAVE - 1);
 	const uint32_t wave = threadIdx.x >> 6;
@@ -1902,8 +2031,9 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 	for (uint32_t i = threadIdx.x; i < 256u; i += NW * WAVE)
 		s_l4[i] = c_l4tab.v[i];
 	if constexpr (CK) {
-		for (uint32_t i = threadIdx.x; i < 1024u; i += NW * WAVE)
-			s_crc[i] = c_crc32c.t[i >> 8][i & 0xffu];
+		for (uint32_t i = threadIdx.x; i < 1024u + CRC_ZN + 64u; i += NW * WAVE)
+			s_crc[i] = i < 1024u ? c_crc32c.t[i >> 8][i & 0xffu]
+				 : (i < 1024u + CRC_ZN ? c_crc32c.z[i - 1024u] : c_crc32c.y[i - 1024u - CRC_ZN]);
 	}
 	for (uint32_t r = WIN / 4; r < WROWS; ++r)
 		W[r * RS + lane] = 0u;   // pad / zero rows: always zero

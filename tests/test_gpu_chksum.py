@@ -121,3 +121,27 @@ def test_checksum_valid_mixed_lengths(built, gpu, ipver):
     assert ((got["in_flags"] >> 31) & 1).all()
     assert np.array_equal(l4_err, bad)
     both(prog, b, CK.ALL_CK | CK.ALL_DROP, f"valid ipv{ipver} drop")
+
+
+def test_sctp_crc_long_frames(built, gpu):
+    """SCTP CRC-32C on both paths: frames up to 16 KB of L4 bytes (the
+    wave-cooperative CRC over 64-B pieces) and longer ones (one lane per
+    frame), valid and with one flipped byte, at odd lengths and unaligned
+    piece boundaries: GPU == oracle, verdicts as constructed."""
+    rng = np.random.default_rng(77)
+    lens = np.array([60, 98, 99, 1514, 9001, 16400, 16417, 16418, 20000, 40001, 65535, 131] * 6)
+    n = lens.size
+    b = pg.build_batch(lens, ipver=np.full(n, 4), l4proto=np.full(n, pg.IPPROTO_SCTP),
+                       sip4=rng.integers(0, 2**32, n).astype(np.uint64),
+                       dip4=rng.integers(0, 2**32, n).astype(np.uint64),
+                       sport=rng.integers(1, 65535, n), dport=rng.integers(1, 65535, n), seed=5)
+    pg.set_checksums(b)
+    bad = np.zeros(n, bool)
+    for i in range(0, n, 2):
+        o, ln = int(b.off[i]), int(b.len[i])
+        if ln > 34 + 20:
+            b.buf[o + int(rng.integers(34 + 12, ln))] ^= 0x81
+            bad[i] = True
+    got = both([R.cos("d", queue=1), ("default", 0)], b, CK.SCTP_CK, "sctp long")
+    assert ((got["in_flags"] >> 31) & 1).all()
+    assert np.array_equal((got["err"] & CK.E_L4CK) != 0, bad)
