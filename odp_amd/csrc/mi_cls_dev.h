@@ -1876,6 +1876,18 @@ __device__ __forceinline__ void zero_tail(uint32_t *W, uint32_t lane, uint32_t l
 	W[min(r0 + 2u, (uint32_t)(WIN / 4)) * RS + lane] = 0u;
 }
 
+// Packet descriptors are read once; DESC_NT=1 loads them nontemporal (A/B:
+// within noise, so the default keeps plain loads).
+#ifndef DESC_NT
+#define DESC_NT 0
+#endif
+template <typename T> __device__ __forceinline__ uint32_t ld_desc(const T *p)
+{
+	if (DESC_NT)
+		return (uint32_t)__builtin_nontemporal_load(p);
+	return (uint32_t)*p;
+}
+
 // One 16-B result record (a coalesced dwordx4 store per lane), nontemporal:
 // the records are not read again by this kernel, and streaming them out
 // instead of leaving 16 MB of dirty lines in L2 for the end-of-kernel
@@ -1975,12 +1987,12 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 	{
 		const uint32_t p0 = tile * WAVE + lane, p1 = (tile + tstride) * WAVE + lane;
 		if (tile < nt && p0 < a.n) {
-			d_off = a.off[p0];
-			d_len = a.len[p0];
+			d_off = ld_desc(a.off + p0);
+			d_len = ld_desc(a.len + p0);
 		}
 		if (tile + tstride < nt && p1 < a.n) {
-			n_off = a.off[p1];
-			n_len = a.len[p1];
+			n_off = ld_desc(a.off + p1);
+			n_len = ld_desc(a.len + p1);
 		}
 	}
 	// Software pipeline over this wave's tiles (64 packets each): while tile
@@ -2072,8 +2084,8 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 			n_off = 0;
 			n_len = 0;
 			if (t2 < nt && p2 < a.n) {
-				n_off = a.off[p2];
-				n_len = a.len[p2];
+				n_off = ld_desc(a.off + p2);
+				n_len = ld_desc(a.len + p2);
 			}
 			// no loads for a tile past the end (its registers would be
 			// waited for before reuse after the loop)
