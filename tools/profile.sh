@@ -10,11 +10,12 @@ TAG=${1:-r02}
 CFG=${2:-3}
 N=${3:-1000000}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
-OUT=$ROOT/gpurun_out/prof_${TAG}_c${CFG}
+OUT=$ROOT/gpurun_out/prof_${TAG}_c${CFG}${PROF_SUFFIX}
 mkdir -p "$OUT"
 cd /tmp
 export TMPDIR=/tmp
-ARGS="--config $CFG --n $N --steps 20 --warmup 5 --timed-only"
+# PROF_EXTRA: more bench arguments (e.g. "--pktin-opt 0x3C" for the checksum path)
+ARGS="--config $CFG --n $N --steps 20 --warmup 5 --timed-only $PROF_EXTRA"
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o kt \
   -- python3 "$ROOT/bench.py" $ARGS > "$OUT/kt.log" 2>&1 || { echo "kt failed"; exit 1; }
 i=0
