@@ -533,9 +533,9 @@ __device__ __forceinline__ uint32_t ck_sum_wave(__amdgpu_buffer_rsrc_t rs, uint3
 		const int32_t hb = (int32_t)(pr >> 6) - (int32_t)(64u * q);
 		u32x4 v[4];
 #pragma unroll
-		for (int32_t k = 0; k < 4; ++k)
-			v[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, (live && 16 * k < hb) ? ob + 16u * k
-											 : OOB_OFF, 0, 0);
+		for (int32_t k = 0; k < 4; ++k)   // only 16-B parts that reach into [from, to)
+			v[k] = __builtin_amdgcn_raw_buffer_load_b128(
+				rs, (live && 16 * k < hb && 16 * k + 16 > lb) ? ob + 16u * k : OOB_OFF, 0, 0);
 		const bool ph = live && lb > 0 && (lb & 3) != 0;
 		const bool pt = live && hb < 64 && (hb & 3) != 0;
 		const uint32_t xh = __builtin_amdgcn_raw_buffer_load_b32(
