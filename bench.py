@@ -406,14 +406,43 @@ def bench_cfg(cls, cfg, a, dev, local, steps, warmup, pktin_opt=0, parity=True, 
     return e
 
 
+def launch_ranks(n):
+    """`bench.py --gpus N` started without a launcher: start one fresh worker
+    process per GPU (torch.distributed.run, rendezvous on 127.0.0.1) and
+    return its exit code.  Runs before this process touches the GPU (only
+    torch.cuda.device_count(), which does not initialise it); fails loudly
+    when fewer than N devices are visible (BENCH_SAME_DEVICE=1 rehearses N
+    ranks on one device)."""
+    import socket
+    import subprocess
+    import torch
+    have = torch.cuda.device_count()
+    if have < n and not os.environ.get("BENCH_SAME_DEVICE"):
+        print(f"bench.py: --gpus {n} requested but {have} GPU(s) visible", file=sys.stderr)
+        return 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
+           str(n), "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     a = parse_args()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(launch_ranks(a.gpus))
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
     if os.environ.get("BENCH_SAME_DEVICE"):   # multi-rank rehearsal on one GPU (tests)
         local = 0
     dist_on = world > 1

@@ -68,10 +68,16 @@ def build(force: bool = False, out_dir: str = PKG, defines=()) -> list[str]:
                  "-I", SRC] + [f"-D{d}" for d in defines]
         objs = []
         jobs = []
+        # MI_CLS_ONLY=kf,k4 (variant builds only): compile just those kernel
+        # translation units; the others become -ENOSYS stubs (mi_cls_dev.h)
+        only = os.environ.get("MI_CLS_ONLY", "") if defines else ""
+        keep = {f"mi_cls_{k}.hip" for k in only.split(",") if k}
         for src in [mi_src] + k_srcs:
             obj = os.path.join(tmp, os.path.basename(src) + ".o")
             objs.append(obj)
-            jobs.append([HIPCC] + flags + ["-c", "-o", obj, src])
+            stub = ["-DMI_CLS_STUB"] if keep and src != mi_src and \
+                os.path.basename(src) not in keep else []
+            jobs.append([HIPCC] + flags + stub + ["-c", "-o", obj, src])
         with cf.ThreadPoolExecutor(max_workers=len(jobs)) as ex:
             list(ex.map(_run, jobs))
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", mi_so] + objs)

@@ -5,6 +5,8 @@
 // mi_cls_k4/8/12/16.hip.
 #include "mi_cls_dev.h"
 
+#include <thread>
+
 // ------------------------------------------------------------------- host
 struct mi_cls_ctx {
 	int device;
@@ -1182,7 +1184,11 @@ static const void *dev_view(const void *p)
 	return (const uint8_t *)a.devicePointer + ((const uint8_t *)p - (const uint8_t *)a.hostPointer);
 }
 
-static int host_launch(mi_cls_ctx_t *c, const uint8_t *pkts, size_t lo, size_t hi,
+// `lim` is the size of the caller's buffer at `pkts`: the zero-copy path is
+// taken only when every frame's last 16-B piece (the kernel reads frames in
+// 16-B pieces from their start) lies inside it; otherwise the frames are
+// staged into the padded device buffer.
+static int host_launch(mi_cls_ctx_t *c, const uint8_t *pkts, size_t lo, size_t hi, size_t lim,
 		       const uint32_t *off, const uint16_t *len, uint32_t n, mi_cls_result_t *out)
 {
 	HIP_OK(hipSetDevice(c->device));
@@ -1194,6 +1200,9 @@ static int host_launch(mi_cls_ctx_t *c, const uint8_t *pkts, size_t lo, size_t h
 	// straight into page-locked `out`.
 	const void *zp = dev_view(pkts), *zo = zp ? dev_view(off) : nullptr;
 	const void *zl = zo ? dev_view(len) : nullptr;
+	for (uint32_t i = 0; zl && i < n; ++i)
+		if ((size_t)off[i] + (((size_t)len[i] + 15u) & ~(size_t)15u) > lim)
+			zl = nullptr;
 	if (zl) {
 		mi_cls_result_t *o = out ? out : n <= c->n_cap ? c->h_out : nullptr;
 		const void *zr = o ? dev_view(o) : nullptr;
@@ -1269,7 +1278,7 @@ extern "C" int mi_cls_classify_host(mi_cls_ctx_t *c, const uint8_t *pkts, size_t
 	for (uint32_t i = 0; i < n; ++i)
 		if ((size_t)off[i] + len[i] > bytes)
 			return -EINVAL;
-	int rc = host_launch(c, pkts, 0, bytes, off, len, n, out);
+	int rc = host_launch(c, pkts, 0, bytes, bytes, off, len, n, out);
 	if (rc)
 		return rc;
 	HIP_OK(hipStreamSynchronize(c->stream));
@@ -1299,7 +1308,7 @@ extern "C" int mi_cls_classify_host_submit(mi_cls_ctx_t *c, const uint8_t *pkts,
 		HIP_OK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
 	else
 		HIP_OK(hipEventSynchronize(*ev));   // ticket t - 8: done before its slot is reused
-	int rc = host_launch(c, pkts, 0, bytes, off, len, n, out);
+	int rc = host_launch(c, pkts, 0, bytes, bytes, off, len, n, out);
 	if (rc)
 		return rc;
 	HIP_OK(hipEventRecord(*ev, c->stream));
@@ -1448,33 +1457,58 @@ extern "C" int mi_cls_group_classify_host(mi_cls_group_t *g, const uint8_t *pkts
 	int rc = mi_cls_shard(len, n, g->n, g->begin);
 	if (rc)
 		return rc;
-	// every device's slice in flight before any wait
-	int first_err = 0;
-	for (uint32_t k = 0; k < g->n && !first_err; ++k) {
+	// every device's slice in flight before any wait.  Page-locked batches
+	// are read in place (host_launch only enqueues work), so one thread
+	// launches every slice; a pageable batch is staged by a copy the HIP
+	// runtime performs synchronously, so each device gets its own host
+	// thread and the slices' copies run side by side.
+	int err[MI_GROUP_MAX] = { 0 };
+	auto run = [&](uint32_t k, bool wait) {
 		const uint32_t b = g->begin[k], e = g->begin[k + 1];
 		if (b == e)
-			continue;
+			return;
 		size_t lo = off[b], hi = 0;
 		for (uint32_t i = b; i < e; ++i) {
 			lo = off[i] < lo ? off[i] : lo;
 			hi = (size_t)off[i] + len[i] > hi ? (size_t)off[i] + len[i] : hi;
 		}
 		lo &= ~(size_t)15;   // keep the slice's 16-B alignment
-		first_err = host_launch(g->ctx[k], pkts, lo, hi, off + b, len + b, e - b, nullptr);
-	}
-	for (uint32_t k = 0; k < g->n; ++k) {
-		const uint32_t b = g->begin[k], e = g->begin[k + 1];
-		if (b == e || !g->ctx[k]->stream)
-			continue;
+		err[k] = host_launch(g->ctx[k], pkts, lo, hi, bytes, off + b, len + b, e - b, nullptr);
+		if (err[k] || !wait)
+			return;
 		if (hipSetDevice(g->ctx[k]->device) != hipSuccess ||
 		    hipStreamSynchronize(g->ctx[k]->stream) != hipSuccess) {
-			first_err = first_err ? first_err : -EIO;
-			continue;
+			err[k] = -EIO;
+			return;
 		}
-		if (!first_err)
+		memcpy(out + b, g->ctx[k]->h_out, (size_t)(e - b) * sizeof(mi_cls_result_t));
+	};
+	if (dev_view(pkts) || g->n == 1) {
+		for (uint32_t k = 0; k < g->n; ++k)
+			run(k, false);
+		for (uint32_t k = 0; k < g->n; ++k) {
+			const uint32_t b = g->begin[k], e = g->begin[k + 1];
+			if (b == e || err[k])
+				continue;
+			if (hipSetDevice(g->ctx[k]->device) != hipSuccess ||
+			    hipStreamSynchronize(g->ctx[k]->stream) != hipSuccess) {
+				err[k] = -EIO;
+				continue;
+			}
 			memcpy(out + b, g->ctx[k]->h_out, (size_t)(e - b) * sizeof(mi_cls_result_t));
+		}
+	} else {
+		std::vector<std::thread> th;
+		for (uint32_t k = 1; k < g->n; ++k)
+			th.emplace_back(run, k, true);
+		run(0, true);
+		for (auto &t : th)
+			t.join();
 	}
-	return first_err;
+	for (uint32_t k = 0; k < g->n; ++k)
+		if (err[k])
+			return err[k];
+	return 0;
 }
 
 // pktin options for the following classify calls: odp_pktin_config_opt_t

@@ -2365,3 +2365,11 @@ int mi_cls_launch_flat(int nw, int fm, unsigned grid, size_t dyn, hipStream_t st
 // pktin-option kernels (CK; NW 4 or 16): mi_cls_kc.hip
 int mi_cls_launch_ck(int nw, bool lt, bool div, unsigned grid, size_t dyn, hipStream_t st,
 		     const KArgs &a);
+
+// Variant builds for A/B runs (odp_amd/_build.py, MI_CLS_ONLY): translation
+// units outside the selected set are compiled with MI_CLS_STUB, so their
+// launchers instantiate no kernel and fail with -ENOSYS.
+#ifdef MI_CLS_STUB
+#undef hipLaunchKernelGGL
+#define hipLaunchKernelGGL(...) return -ENOSYS
+#endif

@@ -74,6 +74,7 @@ typedef struct {
 	int n;
 	int pending;            /* staged (and submitted), not delivered */
 	uint64_t ticket;        /* odp_amd_cls_classify_host_submit, 0 = done */
+	uint64_t gen;           /* control-plane generation the set was submitted under */
 } rx_set_t;
 
 typedef struct {
@@ -1025,9 +1026,9 @@ static void cos_enq_run(odp_packet_t pk[], int num)
 	pkt_hdr_t *h = rt_pkt_hdr(pk[0]);
 	const uint32_t cos = h->cos;
 	odp_queue_t dst = h->dst_queue;
-	odp_pool_t vpool;
-	uint32_t vmax;
-	int use_aggr;
+	odp_pool_t vpool = ODP_POOL_INVALID;
+	uint32_t vmax = 0;
+	int use_aggr = 0;
 	const int std = odp_amd_cls_cos_enq_mode(cos, &vpool, &vmax, &use_aggr);
 
 	if (num < 2 || std != 0) {
@@ -1061,7 +1062,9 @@ static int stage_frames(rt_pktio_t *e, rx_set_t *s, uint32_t max)
 		return -1;
 	s->base = s->stage;
 	if (e->drv == DRV_PCAP) {
-		const int in_place = e->fbuf_pinned;
+		/* in place only when the descriptor / record arrays are page-locked
+		 * too: otherwise mi_cls stages the whole frame store every burst */
+		const int in_place = e->fbuf_pinned && s->arr_pinned;
 
 		if (in_place)
 			s->base = e->fbuf;
@@ -1176,6 +1179,7 @@ static int rx_classify(rt_pktio_t *e, rx_set_t *s, int pipe)
 	s->pending = 1;
 	if (e->parse_layer == ODP_PROTO_LAYER_NONE)
 		return 0;
+	s->gen = odp_amd_cls_generation();
 	if (pipe)
 		rc = odp_amd_cls_classify_host_submit(e->hdl, s->base, s->bytes, s->soff, s->slen,
 						      (uint32_t)s->n, s->res, &s->ticket);
@@ -1201,6 +1205,20 @@ static int rx_finish(rt_pktio_t *e, rx_set_t *s, odp_packet_t out[], int max_out
 		int rc = odp_amd_cls_classify_host_wait(e->hdl, s->ticket);
 
 		s->ticket = 0;
+		if (rc) {
+			rx_drop(e, s, rc);
+			return 0;
+		}
+	}
+	/* The control plane changed while the burst was in flight (a CoS
+	 * destroyed, its queues or pool changed, PMRs added or removed): its
+	 * records name CoS indexes of the old rule snapshot, so classify it again
+	 * under the current one -- what the synchronous path, which has no gap
+	 * between classify and enqueue, would deliver on this call. */
+	if (layer != ODP_PROTO_LAYER_NONE && e->cls_enabled && s->gen != odp_amd_cls_generation()) {
+		int rc = odp_amd_cls_classify_host(e->hdl, s->base, s->bytes, s->soff, s->slen,
+						   (uint32_t)s->n, s->res, 0);
+
 		if (rc) {
 			rx_drop(e, s, rc);
 			return 0;
@@ -1358,7 +1376,9 @@ static int pktio_recv(rt_pktio_t *e, odp_packet_t out[], int max_out)
 	if (p->pending)
 		num_rx += rx_finish(e, p, out, max_out);
 	if (n > 0) {
-		if (pipe && rx_more(e))
+		/* only a burst really in flight waits (a multi-GPU pktio's submit
+		 * completes before it returns: ticket 0) */
+		if (pipe && s->ticket && rx_more(e))
 			e->cur ^= 1;   /* s stays in flight: the next call stages into p */
 		else
 			num_rx += rx_finish(e, s, out + num_rx, max_out - num_rx);

@@ -24,6 +24,9 @@
  *   Q <cos> <slot> <packets> <discards>     (odp_cls_queue_stats)
  * RX_COUNT_ONLY=1: no P lines; "R <packets delivered> <ns>" (receive-path
  *   rate, bench.py's runtime e2e: from odp_pktio_start to the last packet).
+ * RX_SWITCH_RULES=<rules file> (direct mode): replayed after the first
+ *   odp_pktin_recv call, while that call's burst is still in flight on the
+ *   GPU (control-plane change between two receive calls).
  */
 #define _GNU_SOURCE
 #include <inttypes.h>
@@ -392,8 +395,19 @@ int main(int argc, char *argv[])
 
 		if (odp_pktin_queue(pktio, &inq, 1) != 1)
 			return 11;
+		const char *sw = getenv("RX_SWITCH_RULES");
+
 		while (idle < 3) {
 			n = odp_pktin_recv(inq, pk, 512);
+			if (sw) {
+				FILE *f = fopen(sw, "r");
+
+				if (!f)
+					return 7;
+				replay(f, pktio, cos_pools);
+				fclose(f);
+				sw = NULL;
+			}
 			for (int i = 0; i < n; i++) {
 				print_pkt("pktin", pk[i]);
 				odp_packet_free(pk[i]);

@@ -92,3 +92,43 @@ def test_bench_two_ranks_one_device(built, gpu):
     assert line["n_gpus"] == 2 and line["value"] > 0
     assert line["config"]["parallelism"] == "shard2"
     assert line["parity_vs_oracle"] is True
+
+
+def test_bench_gpus_2_self_launch_one_device(built, gpu):
+    """`bench.py --gpus 2` without a launcher starts its own two ranks
+    (BENCH_SAME_DEVICE rehearses them on one device) and reports n_gpus 2."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(BENCH_DIST_BACKEND="gloo", BENCH_SAME_DEVICE="1")
+    r = subprocess.run([sys.executable, os.path.join(H.ROOT, "bench.py"), "--gpus", "2",
+                        "--steps", "3", "--warmup", "1", "--packets", "100000", "--config", "2",
+                        "--no-parity"],
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=240,
+                       env=env, cwd=H.ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["config"]["parallelism"] == "shard2"
+
+
+@pytest.mark.parametrize("ngroup", [1, 3])
+def test_group_host_batch_timing(built, gpu, ngroup):
+    """The group path on a pageable host batch (config 3, 200 k IMIX
+    packets): each device's slice is staged from its own host thread, so the
+    slices' copies do not serialise; records equal the oracle's.  Prints the
+    per-call time (1 and 3 contexts on the one device here)."""
+    import time
+    from odp_amd.cls import Classifier
+    b, prog = R.config3(200_000)
+    exp, _ = oracle_run(prog, b)
+    c = Classifier(gpus=[0] * ngroup)
+    try:
+        c.apply(prog)
+        got = c.classify_host(b)
+        t0 = time.perf_counter()
+        for _ in range(5):
+            got = c.classify_host(b)
+        dt = (time.perf_counter() - t0) / 5
+    finally:
+        c.close()
+    assert_same(got, exp, b, f"{ngroup} contexts")
+    print(f"group classify_host: {ngroup} context(s), {b.n} packets, {dt * 1e3:.2f} ms per call, "
+          f"{b.n / dt / 1e6:.1f} Mpkt/s")

@@ -233,3 +233,27 @@ def test_rx_small_first_segment(built, gpu, tmp_path):
                else H.run_driver("loop", rules, "sched", 4, 1, 1, src=pc, env=env))
         H.compare(got, H.expected(prog, frames, 1, 1, 4))
         assert len(got[0]["deep"]) == 1
+
+
+def test_rx_cos_destroyed_while_burst_in_flight(built, gpu, tmp_path):
+    """A hash-queue CoS is destroyed (and a new default CoS set) between two
+    odp_pktin_recv calls while the first call's burst is still in flight on
+    the GPU.  That burst was classified under the old rule snapshot; it must
+    be delivered under the current one (as the synchronous path would), not
+    to the destroyed CoS's queues: every packet reaches the new CoS, none is
+    discarded."""
+    frames = H.pcap_frames([f for _, f in zoo.all_frames()])
+    pc = str(tmp_path / "in.pcap")
+    H.write_pcap(pc, frames)
+    before = [R.cos("A", num_queue=4, hash_proto=0x7), ("default", 0)]
+    after = [R.cos("B"), ("default", 1), ("cos_destroy", 0)]
+    r1, r2 = str(tmp_path / "r1.txt"), str(tmp_path / "r2.txt")
+    H.write_rules(r1, before)
+    H.write_rules(r2, after)
+    # 3 loops over the capture in bursts of 16: the first call's burst stays
+    # in flight (more frames are waiting at the driver)
+    got = H.run_driver(f"pcap:in={pc}:loops=3", r1, "direct", 4, 1, 1,
+                       env={"ODP_AMD_RX_BURST": "16", "RX_SWITCH_RULES": r2})
+    exp = H.expected(before + after, frames * 3, 1, 1, 4)
+    H.compare(got, exp)
+    assert got[1][2] == 0, got[1]   # in_discards

@@ -100,3 +100,32 @@ def test_two_rank_shards_equal_single(built):
         exp, _ = oracle_run(prog, batch)
         assert np.array_equal(got, exp)
         assert tmax == 2.0
+
+
+def test_bench_gpus_n_without_launcher_fails_loudly_without_devices():
+    """`bench.py --gpus 2` started without torchrun spawns one worker per
+    GPU itself; with fewer devices visible (none here) it must exit non-zero
+    instead of printing a 1-GPU line for a 2-GPU request."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "BENCH_SAME_DEVICE")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
+                        "--steps", "1", "--warmup", "0"], stdout=subprocess.PIPE,
+                       stderr=subprocess.PIPE, text=True, timeout=120, env=env)
+    assert r.returncode != 0
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert "--gpus 2 requested" in r.stderr
+
+
+def test_bench_world_size_mismatch_fails():
+    """Under a launcher, --gpus must equal WORLD_SIZE."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
+                        "--steps", "1", "--warmup", "0"], stdout=subprocess.PIPE,
+                       stderr=subprocess.PIPE, text=True, timeout=120, env=env)
+    assert r.returncode == 2 and "WORLD_SIZE=1" in r.stderr
