@@ -22,7 +22,9 @@
 #ifndef MI_CLS_H_
 #define MI_CLS_H_
 
+#ifndef __HIPCC_RTC__
 #include <stddef.h>
+#endif
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -215,6 +217,22 @@ int mi_cls_classify_host_submit(mi_cls_ctx_t *ctx, const uint8_t *pkts_host, siz
 				mi_cls_result_t *out_host, uint64_t *ticket);
 int mi_cls_classify_host_wait(mi_cls_ctx_t *ctx, uint64_t ticket);
 
+/* Program-specialised kernel of the loaded rules.  A flat program (every
+ * packet decided on the default CoS in one round) gets a kernel whose
+ * classification block is compiled in as constants (hipRTC, in the
+ * background after mi_cls_rules_load; launches use the generic kernel until
+ * it is ready -- the records are the same either way).  Blocks until the
+ * compilation of the loaded program's kernel has ended: 0 = the specialised
+ * kernel is in use, 1 = none (not a flat program, disabled by MI_CLS_JIT=0,
+ * or it failed to compile), -EINVAL = no rules loaded. */
+int mi_cls_spec_wait(mi_cls_ctx_t *ctx);
+
+/* Host-only (no device needed): compile the specialised kernel of a
+ * compiled table's program for block shape nw (4, 12, 16) synchronously.
+ * 0 compiled, 1 not a flat program, < 0 error (-ENOEXEC: the compile
+ * failed).  Tests use it to check the embedded kernel sources build. */
+int mi_cls_spec_compile(const void *tbl, size_t bytes, int nw);
+
 /* ------------------------------------------------------------------------
  * Multi-GPU: one host batch over several devices.
  * The batch shards with no exchange step: mi_cls_shard cuts it into
@@ -278,8 +296,9 @@ int mi_cls_stats_reset(mi_cls_ctx_t *ctx);
  * the per-lane "hot" region (copied to LDS when it fits), [2] CoS with a
  * classification block, [3..6] blocks per engine (direct, candidate,
  * bitmap, wide bitmap), [7] 1 if some rule leads to a CoS with rules,
- * [8] single-candidate blocks.  n >= 9.  Used by tests and tools to check
- * engine selection on the CPU. */
+ * [8] single-candidate blocks, [9] (when n >= 10) 0 if the program is not
+ * flat (decided on the default CoS in one round), else its engine + 1.
+ * n >= 9.  Used by tests and tools to check engine selection on the CPU. */
 int mi_cls_program_info(const void *tbl, size_t bytes, uint32_t *info, uint32_t n);
 
 /* Last error string for the context (static storage, never NULL). */

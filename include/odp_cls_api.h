@@ -301,6 +301,10 @@ int odp_amd_cls_classify_host_submit(odp_pktio_t pktio, const uint8_t *pkts, siz
 				     const uint32_t *off, const uint16_t *len, uint32_t n,
 				     void *out, uint64_t *ticket);
 int odp_amd_cls_classify_host_wait(odp_pktio_t pktio, uint64_t ticket);
+/* Snapshot the current rules into the pktio's GPU context(s) and wait for
+ * their program-specialised kernel (mi_cls_spec_wait): 0 in use, 1 none,
+ * < 0 error. */
+int odp_amd_cls_spec_wait(odp_pktio_t pktio);
 
 /* Create the device context, upload the current rule snapshot and run a
  * warm-up launch (odp_pktio_start). */

@@ -56,16 +56,17 @@ def build(force: bool = False, out_dir: str = PKG, defines=()) -> list[str]:
                       os.path.join(SRC, "odp_rt_internal.h")]
     built = []
     mi_hdr = os.path.join(SRC, "mi_cls_dev.h")
-    k_srcs = [os.path.join(SRC, f"mi_cls_k{w}.hip") for w in (4, 8, 12, 16, "f", "f12", "f16", "c4",
+    k_srcs = [os.path.join(SRC, f"mi_cls_k{w}.hip") for w in (4, 8, 12, 16, "f", "f12", "f16", "c4", "s",
                                                               "c16")]
-    if force or defines or _stale(mi_so, [mi_src, mi_hdr] + k_srcs + hdrs):
+    if force or defines or _stale(mi_so, [mi_src, mi_hdr] + k_srcs + hdrs + [__file__]):
         # one translation unit per block shape + the host code, compiled in
         # parallel (the kernel instantiations dominate the build time)
         import concurrent.futures as cf
         import tempfile
         tmp = tempfile.mkdtemp(prefix="mi_cls_obj_")
         flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-I", INC,
-                 "-I", SRC] + [f"-D{d}" for d in defines]
+                 "-I", SRC, "-I", tmp] + [f"-D{d}" for d in defines]
+        write_src_inc(os.path.join(tmp, "mi_cls_src.inc"), defines)
         objs = []
         jobs = []
         # MI_CLS_ONLY=kf,k4 (variant builds only): compile just those kernel
@@ -80,7 +81,8 @@ def build(force: bool = False, out_dir: str = PKG, defines=()) -> list[str]:
             jobs.append([HIPCC] + flags + stub + ["-c", "-o", obj, src])
         with cf.ThreadPoolExecutor(max_workers=len(jobs)) as ex:
             list(ex.map(_run, jobs))
-        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", mi_so] + objs)
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", mi_so] + objs +
+             ["-lhiprtc"])
         shutil.rmtree(tmp, ignore_errors=True)
         built.append(mi_so)
     if force or _stale(odp_so, odp_srcs + [mi_so] + rt_hdrs):
@@ -98,6 +100,23 @@ def build(force: bool = False, out_dir: str = PKG, defines=()) -> list[str]:
             if b:
                 built.append(b)
     return built
+
+
+def write_src_inc(path, defines=()):
+    """The kernel sources as C string literals for hipRTC (program-specialised
+    kernels, mi_cls.hip): mi_cls.h, mi_cls_dev.h and the build's -D options,
+    so a specialised kernel is compiled from exactly the code of this build."""
+    def lit(name, text):
+        assert ")MICLS\"" not in text
+        return f'static const char {name}[] = R"MICLS({text})MICLS";\n'
+    with open(os.path.join(INC, "mi_cls.h")) as f:
+        h = f.read()
+    with open(os.path.join(SRC, "mi_cls_dev.h")) as f:
+        dev = f.read()
+    defs = ", ".join(f'"-D{d}"' for d in defines)
+    with open(path, "w") as f:
+        f.write(lit("mi_cls_src_h", h) + lit("mi_cls_src_dev", dev) +
+                f"static const char *const mi_cls_src_defs[] = {{ {defs}{', ' if defs else ''}nullptr }};\n")
 
 
 TEST_BIN = os.path.join(ROOT, "tests", "_bin")

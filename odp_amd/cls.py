@@ -141,6 +141,8 @@ def _load():
         "odp_amd_cls_queue_of": (vp, [u32, u32]),
         "odp_amd_cls_generation": (C.c_uint64, []),
         "odp_amd_cls_pktin_opt_set": (i32, [vp, C.c_uint64]),
+        "odp_amd_cls_spec_wait": (i32, [vp]),
+        "mi_cls_spec_wait": (i32, [vp]),
         "mi_cls_device_count": (i32, []),
         "mi_cls_ctx_create": (i32, [i32, C.POINTER(vp)]),
         "mi_cls_ctx_destroy": (i32, [vp]),
@@ -310,13 +312,22 @@ class Classifier:
     def program_info(self) -> dict:
         """Device encoding of the current rule snapshot (host only)."""
         blob = self.compile()
-        info = (C.c_uint32 * 9)()
-        rc = self.L.mi_cls_program_info(blob, len(blob), info, 9)
+        info = (C.c_uint32 * 10)()
+        rc = self.L.mi_cls_program_info(blob, len(blob), info, 10)
         if rc:
             raise RuntimeError(f"mi_cls_program_info: {rc}")
         return {"words": info[0], "hot_words": info[1], "blocks": info[2],
                 "direct": info[3], "candidate": info[4], "bitmap": info[5], "wide": info[6],
-                "tree": bool(info[7]), "cand1": info[8]}
+                "tree": bool(info[7]), "cand1": info[8], "flat_engine": int(info[9]) - 1}
+
+    def spec_wait(self) -> int:
+        """Snapshot the rules and wait for their program-specialised kernel
+        (odp_amd_cls_spec_wait): 0 in use, 1 none (not a flat program,
+        MI_CLS_JIT=0, or the compile failed)."""
+        rc = self.L.odp_amd_cls_spec_wait(self.pktio)
+        if rc < 0:
+            raise RuntimeError(f"odp_amd_cls_spec_wait: {rc}")
+        return rc
 
     # -- data path -------------------------------------------------------
     def classify_device(self, d_buf, d_off, d_len, n, d_out, stream=0):

@@ -30,20 +30,20 @@
 //     round, per-lane blocks when lanes sit on different CoS.  No MFMA:
 //     this is parse-and-compare.
 #pragma once
+// Under hipRTC (program-specialised kernels, mi_cls_spec.cpp) only the
+// device part is compiled: no host headers.
+#ifndef __HIPCC_RTC__
 #include <hip/hip_runtime.h>
 #include <errno.h>
-#include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#endif
+#include <stdint.h>
 
 #include "mi_cls.h"
 
-#include <algorithm>
 #include <type_traits>
-#include <array>
-#include <map>
-#include <vector>
 
 #define WAVE 64
 #ifndef WIN
@@ -1315,6 +1315,37 @@ struct DescU {
 	// 16 words at hot-region word o (a direct block's shared class record)
 	__device__ __forceinline__ DescV root(uint32_t o) const { return DescU{ h + o, h }.vec(0u); }
 };
+// A classification block known when the kernel is compiled (program-
+// specialised kernels, mi_cls_spec.cpp): S::blk holds the default CoS's block
+// words (header and class records, zero-padded by 16 words) and S::root a
+// direct block's shared class record.  Every read has a constant index once
+// bv_eval's class loop is unrolled, so the block's words fold into the
+// instructions as immediates: no scalar loads, no decode of class records at
+// run time.
+template <typename S> struct DescC {
+	uint32_t o;
+	static constexpr bool per_lane = false;
+	__device__ __forceinline__ uint32_t operator()(uint32_t i) const { return S::blk[o + i]; }
+	__device__ __forceinline__ DescC at(uint32_t o2) const { return DescC{ o + o2 }; }
+	__device__ __forceinline__ DescV vec(uint32_t o2) const
+	{
+		DescV d;
+#pragma unroll
+		for (uint32_t i = 0; i < 16; ++i)
+			d.v[i] = S::blk[o + o2 + i];
+		return d;
+	}
+	__device__ __forceinline__ DescV hdr() const { return vec(0u); }
+	__device__ __forceinline__ DescV vec8(uint32_t o2) const { return vec(o2); }
+	__device__ __forceinline__ DescV root(uint32_t) const
+	{
+		DescV d;
+#pragma unroll
+		for (uint32_t i = 0; i < 16; ++i)
+			d.v[i] = S::root[i];
+		return d;
+	}
+};
 // 16-byte read of the hot region (LDS: ds_read_b128, HBM: global dwordx4);
 // i is a multiple of 4 (hot-region blocks, buckets and rows are 16-B aligned)
 __device__ __forceinline__ u32x4 ld4(lword_t H, uint32_t i)
@@ -1947,7 +1978,9 @@ constexpr int waves_per_eu(int nw)
 // checksum / drop option is set; the other kernels require opt == 0 and carry
 // no option code (the checksum path's registers would otherwise be
 // allocated, and spilled, in every kernel).
-template <bool LT, bool DIV, int NW, int FM = -1, bool CK = false>
+// SPEC (void: none): a program-specialised flat kernel -- the default CoS's
+// block is the compile-time DescC<SPEC> (FM >= 0 required).
+template <bool LT, bool DIV, int NW, int FM = -1, bool CK = false, typename SPEC = void>
 __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KArgs a)
 {
 	__shared__ uint32_t s_win[NW * RS * WROWS];
@@ -2230,7 +2263,10 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 		if (__ballot(pend != 0u) != 0ull) {
 			uint32_t hit = 0, nleaf = 0, nxt = 0, nmark = 0;
 			const bool g = pend != 0u;
-			if constexpr (FM >= 0) {
+			if constexpr (!std::is_void<SPEC>::value) {
+				static_assert(FM >= 0, "specialised kernels are flat");
+				bv_eval<FM>(DescC<SPEC>{ 0u }, H, g, k, p, x, hit, nxt, nmark, nleaf);
+			} else if constexpr (FM >= 0) {
 				bv_eval<FM>(DescU{ hc + d_bv, hc }, H, g, k, p, x, hit, nxt, nmark, nleaf);
 			} else {
 				if (d_bv != 0u && d_nr != 0u)
@@ -2353,6 +2389,7 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 }
 
 
+#ifndef __HIPCC_RTC__
 // Launch one instantiation of the kernel for block shape NW (defined in
 // mi_cls_k<NW>.hip).
 int mi_cls_launch_k4(bool lt, bool div, unsigned grid, size_t dyn, hipStream_t st, const KArgs &a);
@@ -2362,9 +2399,13 @@ int mi_cls_launch_k16(bool lt, bool div, unsigned grid, size_t dyn, hipStream_t 
 // flat-program kernels (FM = engine of the default CoS block; NW 4, 12, 16;
 // hot region in LDS): mi_cls_kf.hip
 int mi_cls_launch_flat(int nw, int fm, unsigned grid, size_t dyn, hipStream_t st, const KArgs &a);
+// a specialised flat kernel compiled into an A/B build (mi_cls_ks.hip)
+int mi_cls_launch_spec(unsigned grid, size_t dyn, hipStream_t st, const KArgs &a);
 // pktin-option kernels (CK; NW 4 or 16): mi_cls_kc.hip
 int mi_cls_launch_ck(int nw, bool lt, bool div, unsigned grid, size_t dyn, hipStream_t st,
 		     const KArgs &a);
+
+#endif   // !__HIPCC_RTC__
 
 // Variant builds for A/B runs (odp_amd/_build.py, MI_CLS_ONLY): translation
 // units outside the selected set are compiled with MI_CLS_STUB, so their

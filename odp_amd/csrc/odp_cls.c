@@ -1417,6 +1417,29 @@ int odp_amd_cls_classify_host_wait(odp_pktio_t h, uint64_t ticket)
 	return e->ctx ? mi_cls_classify_host_wait(e->ctx, ticket) : -EINVAL;
 }
 
+int odp_amd_cls_spec_wait(odp_pktio_t h)
+{
+	pktio_t *e = get_pktio(h);
+	int rc;
+
+	if (!e)
+		return -EINVAL;
+	rc = ensure_ctx(e);
+	if (rc)
+		return rc;
+	rc = sync_rules(e, NULL);
+	if (rc)
+		return rc;
+	if (!e->grp)
+		return mi_cls_spec_wait(e->ctx);
+	for (uint32_t k = 0; k < mi_cls_group_size(e->grp); k++) {
+		rc = mi_cls_spec_wait(mi_cls_group_ctx(e->grp, k));
+		if (rc)
+			return rc;
+	}
+	return 0;
+}
+
 /* pktio start: device context, rule snapshot and a warm-up launch, so the
  * first received burst does not pay for GPU initialisation. */
 int odp_amd_cls_prepare(odp_pktio_t h, int parse_only)

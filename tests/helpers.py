@@ -12,13 +12,18 @@ def oracle_run(prog, batch, limits=(255, 8192, 4096), pktin_opt=0):
     return o.classify(batch), o
 
 
-def gpu_run(prog, batch, limits=(255, 8192, 4096), pktin_opt=0):
+def gpu_run(prog, batch, limits=(255, 8192, 4096), pktin_opt=0, spec=False):
+    """spec: wait for the program-specialised kernel before classifying (a
+    flat program must get one); otherwise whichever kernel is ready."""
     from odp_amd.cls import Classifier
     c = Classifier(gpu=0, limits=limits)
     try:
         c.apply(prog)
         if pktin_opt:
             c.set_pktin_opt(pktin_opt)
+        if spec:
+            rc = c.spec_wait()
+            assert rc == (0 if c.program_info()["flat_engine"] >= 0 else 1), rc
         return c.classify(batch)
     finally:
         c.close()

@@ -27,6 +27,8 @@ ENGINE_ENV = {
     "nocand1": {"MI_CLS_NO_CAND1": "1"},   # no single-candidate engine (wide / lists)
     "noportmerge": {"MI_CLS_NO_PORTMERGE": "1"},   # separate UDP / TCP port classes
     "noflat": {"MI_CLS_NO_FLAT": "1"},   # general kernel for flat programs too
+    "spec": {},                          # program-specialised kernel (waited for)
+    "nojit": {"MI_CLS_JIT": "0"},        # no specialised kernels
 }
 
 
@@ -36,11 +38,11 @@ def both(prog, batch, limits=(255, 8192, 4096), what="", engine="auto"):
     force one of the kernel's paths (ENGINE_ENV)."""
     import os
     keys = ("MI_CLS_NO_BV", "MI_CLS_DIV", "MI_CLS_WPB", "MI_CLS_NO_WIDE", "MI_CLS_NO_CAND1",
-            "MI_CLS_NO_PORTMERGE", "MI_CLS_NO_FLAT")
+            "MI_CLS_NO_PORTMERGE", "MI_CLS_NO_FLAT", "MI_CLS_JIT")
     old = {k: os.environ.pop(k, None) for k in keys}
     os.environ.update(ENGINE_ENV[engine])
     try:
-        got = gpu_run(prog, batch, limits)
+        got = gpu_run(prog, batch, limits, spec=engine == "spec")
     finally:
         for k in keys:
             os.environ.pop(k, None)
@@ -100,7 +102,7 @@ def test_zoo_no_default(built, gpu):
 
 
 @pytest.mark.parametrize("engine", ["auto", "linear", "nodiv", "div", "wpb16", "nowide", "nocand1",
-                                    "noportmerge", "noflat"])
+                                    "noportmerge", "noflat", "spec", "nojit"])
 @pytest.mark.parametrize("seed", range(12))
 def test_random_programs_fuzz(built, gpu, seed, engine):
     rng = np.random.default_rng(1000 + seed)
@@ -114,7 +116,7 @@ def test_random_programs_fuzz(built, gpu, seed, engine):
 
 
 @pytest.mark.parametrize("engine", ["auto", "linear", "nodiv", "wpb4", "wpb16", "nowide", "nocand1",
-                                    "noportmerge", "noflat"])
+                                    "noportmerge", "noflat", "spec", "nojit"])
 @pytest.mark.parametrize("cfg,n", [(1, 10_000), (2, 100_000), (3, 50_000), (4, 50_000),
                                    (5, 20_000)])
 def test_configs_small(built, gpu, cfg, n, engine):
@@ -123,7 +125,7 @@ def test_configs_small(built, gpu, cfg, n, engine):
     assert summary(got)["enq"] > 0
 
 
-@pytest.mark.parametrize("engine", ["auto", "nowide", "div", "nocand1", "noflat"])
+@pytest.mark.parametrize("engine", ["auto", "nowide", "div", "nocand1", "noflat", "spec"])
 @pytest.mark.parametrize("num_rules", [33, 64, 100, 200, 255, 256, 257])
 def test_wide_rule_counts(built, gpu, num_rules, engine):
     """Rule counts around the wide-bitmap engine's word boundaries (33..256
@@ -229,14 +231,23 @@ def test_config3_full_size_properties(built, gpu):
     assert np.array_equal(got, gpu_run(prog, b))
 
 
+@pytest.mark.parametrize("spec", [False, True], ids=["generic", "spec"])
 @pytest.mark.parametrize("cfg,kw", [(3, {}), (3, {"size": 60}), (4, {}), (5, {}), (2, {})],
                          ids=["config3_imix", "config3_64B", "config4", "config5", "config2"])
-def test_configs_full_size(built, gpu, cfg, kw):
+def test_configs_full_size(built, gpu, cfg, kw, spec):
     """BASELINE configs at full size (1 M packets: one GPU's shard for
-    configs 4 and 5): every record bit-exact vs the multithreaded oracle."""
+    configs 4 and 5): every record bit-exact vs the multithreaded oracle,
+    with the generic kernels (MI_CLS_JIT=0) and with the program-specialised
+    kernel (waited for; config 5 is a tree and has none)."""
+    import os
     from oracle.oracle import Oracle
     b, prog = (R.config3(1_000_000, **kw) if cfg == 3 else R.CONFIGS[cfg](1_000_000))
-    got = gpu_run(prog, b)
+    if not spec:
+        os.environ["MI_CLS_JIT"] = "0"
+    try:
+        got = gpu_run(prog, b, spec=spec)
+    finally:
+        os.environ.pop("MI_CLS_JIT", None)
     o = Oracle()
     o.apply(prog)
     exp = o.classify(b, threads=16)
