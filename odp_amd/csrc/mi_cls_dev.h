@@ -1978,8 +1978,8 @@ constexpr int waves_per_eu(int nw)
 // checksum / drop option is set; the other kernels require opt == 0 and carry
 // no option code (the checksum path's registers would otherwise be
 // allocated, and spilled, in every kernel).
-// SPEC (void: none): a program-specialised flat kernel -- the default CoS's
-// block is the compile-time DescC<SPEC> (FM >= 0 required).
+// SPEC (void: none): a program-specialised kernel -- the default CoS's block
+// (evaluated in the first descent round) is the compile-time DescC<SPEC>.
 template <bool LT, bool DIV, int NW, int FM = -1, bool CK = false, typename SPEC = void>
 __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KArgs a)
 {
@@ -2264,7 +2264,8 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 			uint32_t hit = 0, nleaf = 0, nxt = 0, nmark = 0;
 			const bool g = pend != 0u;
 			if constexpr (!std::is_void<SPEC>::value) {
-				static_assert(FM >= 0, "specialised kernels are flat");
+				// the default CoS's block is compiled in (it has one: the
+				// host specialises only such programs)
 				bv_eval<FM>(DescC<SPEC>{ 0u }, H, g, k, p, x, hit, nxt, nmark, nleaf);
 			} else if constexpr (FM >= 0) {
 				bv_eval<FM>(DescU{ hc + d_bv, hc }, H, g, k, p, x, hit, nxt, nmark, nleaf);

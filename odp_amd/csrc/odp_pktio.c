@@ -1359,6 +1359,21 @@ static int pktio_recv(rt_pktio_t *e, odp_packet_t out[], int max_out)
 		rx_prof = getenv("ODP_AMD_RX_PROF") != NULL;
 	if (!e->cls_enabled && (uint32_t)max_out < burst)
 		burst = (uint32_t)max_out;
+	if (e->drv == DRV_PCAP) {
+		/* pcap frames become packets of the pktio's pool at delivery: stage
+		 * no more than the pool can still hold after the burst in flight,
+		 * so a packet allocation never fails on a staged frame (frames not
+		 * staged stay in the store for the next call; the reference instead
+		 * consumes the frame and stops on a failed allocation, pcap.c:324-327) */
+		rt_pool_t *pl = rt_pool(e->pool);
+
+		if (pl) {
+			long room = (long)pl->num_free - (p->pending ? (long)p->n : 0);
+
+			if (room < (long)burst)
+				burst = room > 0 ? (uint32_t)room : 0u;
+		}
+	}
 	uint64_t t0 = prof_ns();
 	int n = stage_frames(e, s, burst);
 	uint64_t t1 = prof_ns();

@@ -337,4 +337,120 @@ def config5(n=1_000_000, rank=0):
     return b, prog
 
 
+def _acl_fields(rules, n, rng, hit_frac, lens):
+    """Per-packet IPv4 fields for rule sets with arbitrary constraints: each
+    rule is a dict of optional constraints sip / dip ((net, plen)), proto,
+    dport, sport, dscp, len; hit_frac of the packets are built to satisfy a
+    random rule's constraints (the fields it leaves open stay random, so a
+    packet may match an earlier rule first -- first-match order decides)."""
+    sip = (_u32(172, 16, 0, 0) | rng.integers(0, 65536, n)).astype(np.uint64)
+    dip = (_u32(192, 168, 0, 0) | rng.integers(0, 65536, n)).astype(np.uint64)
+    proto = np.where(rng.random(n) < 0.8, pg.IPPROTO_UDP, pg.IPPROTO_TCP)
+    dport = rng.integers(20000, 65535, n)
+    sport = rng.integers(1024, 65535, n)
+    dscp = rng.integers(0, 64, n)
+    lens = lens.copy()
+    hit = np.nonzero(rng.random(n) < hit_frac)[0]
+    tgt = rng.integers(0, len(rules), hit.size)
+    host = rng.integers(0, 1 << 16, hit.size).astype(np.uint64)
+    for i, t, h in zip(hit, tgt, host):
+        r = rules[t]
+        for key, arr in (("sip", sip), ("dip", dip)):
+            if key in r:
+                net, plen = r[key]
+                arr[i] = net | (int(h) & ((1 << (32 - plen)) - 1))
+        if "proto" in r:
+            proto[i] = r["proto"]
+        for key, arr in (("dport", dport), ("sport", sport), ("dscp", dscp), ("len", lens)):
+            if key in r:
+                arr[i] = r[key]
+    return sip, dip, proto, dport, sport, dscp, lens
+
+
+def _acl_terms(r):
+    terms = []
+    for key, kind in (("sip", PMR_SIP_ADDR), ("dip", PMR_DIP_ADDR)):
+        if key in r:
+            net, plen = r[key]
+            terms.append(t_ip4(kind, net.to_bytes(4, "big"), plen))
+    if "proto" in r:
+        terms.append(t_u8(PMR_IPPROTO, r["proto"]))
+    tcp = r.get("proto") == pg.IPPROTO_TCP
+    if "dport" in r:
+        terms.append(t_be16(PMR_TCP_DPORT if tcp else PMR_UDP_DPORT, r["dport"]))
+    if "sport" in r:
+        terms.append(t_be16(PMR_TCP_SPORT if tcp else PMR_UDP_SPORT, r["sport"]))
+    if "dscp" in r:
+        terms.append(t_u8(PMR_IP_DSCP, r["dscp"], 0x3F))
+    if "len" in r:
+        terms.append(t_len(r["len"]))
+    return terms
+
+
+def _acl_batch(rules, n, rng, rank, seed, num_dst=32):
+    lens = pg.imix_lens(rng, n)
+    sip, dip, proto, dport, sport, dscp, lens = _acl_fields(rules, n, rng, 0.7, lens)
+    b = pg.build_batch(lens, ipver=np.full(n, 4), l4proto=proto, sip4=sip, dip4=dip,
+                       sport=sport, dport=dport, tos=dscp << 2, seed=seed + rank)
+    prog = [cos("default", queue=1)] + [cos(f"c{i}", queue=100 + i) for i in range(num_dst)]
+    prog.append(("default", 0))
+    for i, r in enumerate(rules):
+        prog.append(("pmr", _acl_terms(r), 0, 1 + i % num_dst, 0))
+    return b, prog
+
+
+def config3_nested(n=1_000_000, rank=0, scale=1):
+    """Config 3 traffic (IMIX IPv4, 70 % aimed at a rule) under an ACL with
+    overlapping rules: 256 PMRs over nested SIP / DIP prefixes, longest
+    first -- 128 /24s (with protocol, half with a destination port), 64 /20s
+    over the same space (protocol only: wildcard ports) and 64 /16s (port
+    only: wildcard protocol) -- so a packet's key values name several rules
+    and first-match order decides (odp_classification.c:1624-1667; the
+    overlapping-PMR series of odp_classification_test_pmr.c:1554-1731).
+    scale=4: 1024 PMRs of the same shapes (past the 256 rules a wide bitmap
+    block holds: candidate lists)."""
+    rng = np.random.default_rng(pg.seed_for(3) + 31 + 7919 * rank)
+    rules = []
+    for k in range(128 * scale):
+        r = {"dip" if k % 3 == 2 else "sip": (_u32(10, 1 + k // 256, k % 256, 0), 24),
+             "proto": pg.IPPROTO_TCP if k % 5 == 0 else pg.IPPROTO_UDP}
+        if k % 2 == 0:
+            r["dport"] = 1000 + k
+        rules.append(r)
+    for j in range(64 * scale):
+        rules.append({"sip" if j % 2 else "dip": (_u32(10, 1 + j // 64, 16 * (j % 16), 0), 20),
+                      "proto": pg.IPPROTO_UDP if (j // 2) % 2 else pg.IPPROTO_TCP})
+    for m in range(64 * scale):
+        rules.append({"dip" if m % 2 else "sip": (_u32(10, 1 + m % (4 * scale), 0, 0), 16),
+                      "dport": 2000 + m})
+    return _acl_batch(rules, n, rng, rank, 31)
+
+
+def config3_classes(n=1_000_000, rank=0):
+    """Config 3 traffic under 256 PMRs spread over 9 key classes (SIP /24,
+    DIP /24, SIP /16, DIP /16, IPPROTO, destination port, source port, DSCP,
+    frame length) -- one more than a classification block holds, so the
+    default CoS falls back to the linear scan."""
+    rng = np.random.default_rng(pg.seed_for(3) + 37 + 7919 * rank)
+    rules = []
+    for i in range(256):
+        k = i // 6
+        t = i % 6
+        if t == 0:
+            r = {"sip": (_u32(10, 2, k, 0), 24), "proto": pg.IPPROTO_UDP, "dport": 3000 + k}
+        elif t == 1:
+            r = {"dip": (_u32(10, 3, k, 0), 24), "sport": 4000 + k}
+        elif t == 2:
+            r = {"sip": (_u32(10, 4 + k % 8, 0, 0), 16), "dscp": k % 64}
+        elif t == 3:
+            r = {"dip": (_u32(10, 12 + k % 8, 0, 0), 16), "proto": pg.IPPROTO_TCP,
+                 "sport": 5000 + k}
+        elif t == 4:
+            r = {"dscp": (k * 7) % 64, "dport": 6000 + k}
+        else:
+            r = {"len": 566, "dport": 7000 + k}
+        rules.append(r)
+    return _acl_batch(rules, n, rng, rank, 37)
+
+
 CONFIGS = {1: config1, 2: config2, 3: config3, 4: config4, 5: config5}

@@ -23,7 +23,8 @@ def gpu_run(prog, batch, limits=(255, 8192, 4096), pktin_opt=0, spec=False):
             c.set_pktin_opt(pktin_opt)
         if spec:
             rc = c.spec_wait()
-            assert rc == (0 if c.program_info()["flat_engine"] >= 0 else 1), rc
+            # a flat program always has one (trees: when the default CoS has a block)
+            assert rc == 0 or (rc == 1 and c.program_info()["flat_engine"] < 0), rc
         return c.classify(batch)
     finally:
         c.close()

@@ -212,21 +212,23 @@ def test_classify_without_gpu_fails_loudly(c):
     assert rc < 0        # -ENODEV: no CPU fallback exists
 
 
-@pytest.mark.parametrize("cfg,flat", [(2, True), (3, True), (4, True), (5, False)])
-def test_specialised_kernel_compiles(built, cfg, flat):
+@pytest.mark.parametrize("cfg,flat,spec", [(2, True, True), (3, True, True), (4, True, True),
+                                           (5, False, True), ("classes", False, False)])
+def test_specialised_kernel_compiles(built, cfg, flat, spec):
     """The embedded kernel sources compile with hipRTC (no GPU needed) into
-    the program-specialised kernel of a flat program; a CoS tree (config 5)
-    has none."""
+    the program-specialised kernel of a program whose default CoS has a
+    classification block (flat programs and CoS trees such as config 5);
+    a default CoS on the linear scan (9 key classes) has none."""
     L = cls.lib()
     L.mi_cls_spec_compile.restype = C.c_int
     L.mi_cls_spec_compile.argtypes = [C.c_void_p, C.c_size_t, C.c_int]
-    b, prog = R.CONFIGS[cfg](100)
+    b, prog = R.config3_classes(100) if cfg == "classes" else R.CONFIGS[cfg](100)
     c = cls.Classifier(gpu=0)
     try:
         c.apply(prog)
         blob = c.compile()
         assert (c.program_info()["flat_engine"] >= 0) == flat
-        for nw in ((4, 16) if cfg == 3 else (4,)):
-            assert L.mi_cls_spec_compile(blob, len(blob), nw) == (0 if flat else 1)
+        for nw in ((4, 16) if cfg == 3 else (16,)):
+            assert L.mi_cls_spec_compile(blob, len(blob), nw) == (0 if spec else 1)
     finally:
         c.close()
