@@ -2400,8 +2400,6 @@ int mi_cls_launch_k16(bool lt, bool div, unsigned grid, size_t dyn, hipStream_t 
 // flat-program kernels (FM = engine of the default CoS block; NW 4, 12, 16;
 // hot region in LDS): mi_cls_kf.hip
 int mi_cls_launch_flat(int nw, int fm, unsigned grid, size_t dyn, hipStream_t st, const KArgs &a);
-// a specialised flat kernel compiled into an A/B build (mi_cls_ks.hip)
-int mi_cls_launch_spec(unsigned grid, size_t dyn, hipStream_t st, const KArgs &a);
 // pktin-option kernels (CK; NW 4 or 16): mi_cls_kc.hip
 int mi_cls_launch_ck(int nw, bool lt, bool div, unsigned grid, size_t dyn, hipStream_t st,
 		     const KArgs &a);
