@@ -217,20 +217,22 @@ int mi_cls_classify_host_submit(mi_cls_ctx_t *ctx, const uint8_t *pkts_host, siz
 				mi_cls_result_t *out_host, uint64_t *ticket);
 int mi_cls_classify_host_wait(mi_cls_ctx_t *ctx, uint64_t ticket);
 
-/* Program-specialised kernel of the loaded rules.  A flat program (every
- * packet decided on the default CoS in one round) gets a kernel whose
- * classification block is compiled in as constants (hipRTC, in the
+/* Program-specialised kernel of the loaded rules.  A program whose default
+ * CoS has a classification block and whose rules do not form a CoS tree
+ * gets a kernel with that block compiled in as constants (hipRTC, in the
  * background after mi_cls_rules_load; launches use the generic kernel until
  * it is ready -- the records are the same either way).  Blocks until the
  * compilation of the loaded program's kernel has ended: 0 = the specialised
- * kernel is in use, 1 = none (not a flat program, disabled by MI_CLS_JIT=0,
- * or it failed to compile), -EINVAL = no rules loaded. */
+ * kernel is in use, 1 = none (no such block, a CoS tree, disabled by
+ * MI_CLS_JIT=0, or it failed to compile), -EINVAL = no rules loaded. */
 int mi_cls_spec_wait(mi_cls_ctx_t *ctx);
 
 /* Host-only (no device needed): compile the specialised kernel of a
- * compiled table's program for block shape nw (4, 12, 16) synchronously.
- * 0 compiled, 1 not a flat program, < 0 error (-ENOEXEC: the compile
- * failed).  Tests use it to check the embedded kernel sources build. */
+ * compiled table's program for block shape nw (4, 12, 16) synchronously
+ * (the tree form for CoS trees, which the data path does not use).
+ * 0 compiled, 1 the default CoS has no classification block, < 0 error
+ * (-ENOEXEC: the compile failed).  Tests use it to check the embedded
+ * kernel sources build. */
 int mi_cls_spec_compile(const void *tbl, size_t bytes, int nw);
 
 /* ------------------------------------------------------------------------
@@ -297,7 +299,9 @@ int mi_cls_stats_reset(mi_cls_ctx_t *ctx);
  * classification block, [3..6] blocks per engine (direct, candidate,
  * bitmap, wide bitmap), [7] 1 if some rule leads to a CoS with rules,
  * [8] single-candidate blocks, [9] (when n >= 10) 0 if the program is not
- * flat (decided on the default CoS in one round), else its engine + 1.
+ * flat (decided on the default CoS in one round), else its engine + 1,
+ * [10] (n >= 11) CoS whose rules need a chain of blocks (more key classes
+ * than one block holds; [2..8] count their first blocks).
  * n >= 9.  Used by tests and tools to check engine selection on the CPU. */
 int mi_cls_program_info(const void *tbl, size_t bytes, uint32_t *info, uint32_t n);
 

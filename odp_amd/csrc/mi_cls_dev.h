@@ -1278,14 +1278,16 @@ __device__ __forceinline__ uint32_t bv_fold(const uint32_t k[4])
 
 // Cuckoo bucket of a key: x = the key word (one-word keys) or bv_fold (longer
 // keys), folded to 24 bits that depend on every key bit, times a 24-bit
-// multiplier; the top 16 bits of the low product word, scaled to [0, nb)
-// (nb <= 65536).  Two v_mul_u32_u24 (full rate, unlike a 32-bit multiply).
+// multiplier; bits 8-23 of the product, scaled to [0, nb) (nb <= 65536).
+// (The product's top bits stay near zero for small keys -- DSCP, IP
+// protocol, small ports -- which then crowd a few buckets; bits 8-23 spread
+// any key set.)  Two v_mul_u32_u24 (full rate, unlike a 32-bit multiply).
 // host_bucket() is the same arithmetic.
 __device__ __forceinline__ uint32_t bv_bucket(uint32_t x, uint32_t m, uint32_t nb)
 {
 	// (__umul24 returns int: shift the unsigned products)
 	const uint32_t h = (uint32_t)__umul24(x ^ (x >> 16), m);
-	return (uint32_t)__umul24(h >> 16, nb) >> 16;
+	return (uint32_t)__umul24((h >> 8) & 0xffffu, nb) >> 16;
 }
 
 // Word readers of a classification block: wave-uniform blocks are read with
@@ -1324,9 +1326,10 @@ struct DescU {
 // run time.
 template <typename S> struct DescC {
 	uint32_t o;
+	cword_t h;              // the hot region (a chain's further blocks, read as DescU)
 	static constexpr bool per_lane = false;
 	__device__ __forceinline__ uint32_t operator()(uint32_t i) const { return S::blk[o + i]; }
-	__device__ __forceinline__ DescC at(uint32_t o2) const { return DescC{ o + o2 }; }
+	__device__ __forceinline__ DescC at(uint32_t o2) const { return DescC{ o + o2, h }; }
 	__device__ __forceinline__ DescV vec(uint32_t o2) const
 	{
 		DescV d;
@@ -1497,38 +1500,15 @@ __device__ __forceinline__ bool split_key(const D &blk, uint32_t ro, bool act, c
 	return bv_key(cr, k, p, x, key);
 }
 
-// Classification block evaluation of one CoS for the lanes in `act`
-// (see build_bv for the two modes).  `blk` reads the CoS's block (wave-
-// uniform or per lane); H is the hot region the block's offsets index.  On
-// return, lanes of `act` with a matching rule have hit = 1 and the rule's
-// destination CoS / mark / leaf bit in nxt / nmark / nleaf.
-// FM >= 0: the block's engine is known at compile time (the flat-program
-// kernels); -1: read from the block.
-template <int FM = -1, typename D, typename T>
-__device__ __forceinline__ void bv_eval(const D &blk, T H, bool act, const Pkt &k, const Parsed &p,
-					const Fields &x, uint32_t &hit, uint32_t &nxt, uint32_t &nmark,
-					uint32_t &nleaf)
+// First holding rule of one non-direct block (modes 1-4) for the lanes in
+// `act` (BV_NONE: none); rule numbers index the block's result words.
+template <int FM, typename D, typename T>
+__device__ __forceinline__ uint32_t bv_first(const D &blk, const DescV &hb, T H, bool act,
+					     const Pkt &k, const Parsed &p, const Fields &x)
 {
-	const auto hb = blk.hdr();   // the block header (words 0-7)
-	const uint32_t mode = FM >= 0 ? (uint32_t)FM : hb(0), ncls = hb(1), res = hb(2);
+	const uint32_t mode = FM >= 0 ? (uint32_t)FM : (hb(0) & 0xffu), ncls = hb(1);
 	uint32_t first = BV_NONE;
-	if (mode == 0u) {
-		// direct: one class, the slot holds the result word of the first
-		// live rule of its key (BV_EMPTY: none); a miss takes the block's
-		// "no term" rule (0: none).  The class record is shared by the
-		// direct blocks with the same class (header word 2); the header
-		// holds the miss word and the table (bucket count, offset, m1, m2)
-		uint32_t key[4], nk;
-		const bool present = split_key(blk, hb(2), act, k, p, x, key, nk);
-		const uint32_t val = bv_probe(H, key, act && present, nk, hb(4), hb(5), hb(6), hb(7));
-		const uint32_t rw = val != 0u ? (val == BV_EMPTY ? 0u : val) : hb(3);
-		const bool h = act && rw != 0u;
-		nxt = h ? (rw & 0xffu) : nxt;
-		nleaf = h ? ((rw >> 8) & 1u) : nleaf;
-		nmark = h ? (rw >> 16) : nmark;
-		hit = h ? 1u : hit;
-		return;
-	} else if (mode == 2u) {
+	if (mode == 2u) {
 		// bitmap: AND of the classes' 32-bit rows and the alive row
 		uint32_t acc = hb(4);
 #pragma unroll
@@ -1720,6 +1700,55 @@ __device__ __forceinline__ void bv_eval(const D &blk, T H, bool act, const Pkt &
 					}
 				}
 			}
+		}
+	}
+	return first;
+}
+
+// Classification block evaluation of one CoS for the lanes in `act`
+// (see build_bv for the two modes).  `blk` reads the CoS's block (wave-
+// uniform or per lane); H is the hot region the block's offsets index.  On
+// return, lanes of `act` with a matching rule have hit = 1 and the rule's
+// destination CoS / mark / leaf bit in nxt / nmark / nleaf.
+// FM >= 0: the block's engine is known at compile time (the flat-program
+// kernels); -1: read from the block.
+// A CoS whose rules need more than BV_MAX_CLS key classes has a chain of
+// blocks (header word 0 = mode | next block << 8), each over a group of its
+// rules with at most BV_MAX_CLS classes and the CoS's rule numbering; the
+// first holding rule is the smallest over the chain.  Chained CoS are
+// evaluated wave-uniformly only (their CoS entry's block word has bit 31
+// set, which the per-lane rounds treat as "no block").
+template <int FM = -1, typename D, typename T>
+__device__ __forceinline__ void bv_eval(const D &blk, T H, bool act, const Pkt &k, const Parsed &p,
+					const Fields &x, uint32_t &hit, uint32_t &nxt, uint32_t &nmark,
+					uint32_t &nleaf)
+{
+	const auto hb = blk.hdr();   // the block header (words 0-7)
+	const uint32_t mode = FM >= 0 ? (uint32_t)FM : (hb(0) & 0xffu), res = hb(2);
+	if (mode == 0u) {
+		// direct: one class, the slot holds the result word of the first
+		// live rule of its key (BV_EMPTY: none); a miss takes the block's
+		// "no term" rule (0: none).  The class record is shared by the
+		// direct blocks with the same class (header word 2); the header
+		// holds the miss word and the table (bucket count, offset, m1, m2)
+		uint32_t key[4], nk;
+		const bool present = split_key(blk, hb(2), act, k, p, x, key, nk);
+		const uint32_t val = bv_probe(H, key, act && present, nk, hb(4), hb(5), hb(6), hb(7));
+		const uint32_t rw = val != 0u ? (val == BV_EMPTY ? 0u : val) : hb(3);
+		const bool h = act && rw != 0u;
+		nxt = h ? (rw & 0xffu) : nxt;
+		nleaf = h ? ((rw >> 8) & 1u) : nleaf;
+		nmark = h ? (rw >> 16) : nmark;
+		hit = h ? 1u : hit;
+		return;
+	}
+	uint32_t first = bv_first<FM>(blk, hb, H, act, k, p, x);
+	if constexpr (FM < 0 && !D::per_lane) {
+		for (uint32_t nx = hb(0) >> 8; nx != 0u;) {
+			const DescU nb{ blk.h + nx, blk.h };
+			const auto nh = nb.hdr();
+			first = min(first, bv_first<-1>(nb, nh, H, act, k, p, x));
+			nx = nh(0) >> 8;
 		}
 	}
 	const bool h = act && first != BV_NONE;
@@ -2008,7 +2037,7 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 	// the default CoS's words (the first descent round always evaluates it)
 	const cword_t dce = hc + COS_WORDS * (uint32_t)max(def_cos, 0);
 	const uint32_t d_nr = def_cos >= 0 ? dce[C_NR] : 0u;
-	const uint32_t d_bv = dce[C_BV], d_rec0 = dce[C_REC0];
+	const uint32_t d_bv = dce[C_BV] & 0x7fffffffu, d_rec0 = dce[C_REC0];   // bit 31: chained
 	const bool stats_on = a.stats != nullptr;
 	typedef typename std::conditional<LT, lword_t, gword_t>::type hot_t;
 	hot_t H;
@@ -2266,7 +2295,7 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 			if constexpr (!std::is_void<SPEC>::value) {
 				// the default CoS's block is compiled in (it has one: the
 				// host specialises only such programs)
-				bv_eval<FM>(DescC<SPEC>{ 0u }, H, g, k, p, x, hit, nxt, nmark, nleaf);
+				bv_eval<FM>(DescC<SPEC>{ 0u, hc }, H, g, k, p, x, hit, nxt, nmark, nleaf);
 			} else if constexpr (FM >= 0) {
 				bv_eval<FM>(DescU{ hc + d_bv, hc }, H, g, k, p, x, hit, nxt, nmark, nleaf);
 			} else {
@@ -2290,7 +2319,8 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 					const uint32_t my_nr = H[ci + C_NR];
 					const uint32_t my_bv = H[ci + C_BV];
 					const bool empty = pend != 0u && my_nr == 0u;
-					const bool bvl = pend != 0u && my_nr != 0u && my_bv != 0u;
+					// chained blocks (bit 31) are evaluated wave-uniformly below
+					const bool bvl = pend != 0u && my_nr != 0u && my_bv != 0u && (my_bv >> 31) == 0u;
 					if (__ballot(bvl))
 						bv_eval(DescL<hot_t>{ H, my_bv, hc }, H, bvl, k, p, x, hit, nxt, nmark,
 							nleaf);
@@ -2305,7 +2335,7 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 				const bool g = act && cur == c1;
 				grp = g ? 1u : 0u;
 				const cword_t ce = hc + COS_WORDS * (uint32_t)c1;
-				const uint32_t nr = ce[C_NR], bv = ce[C_BV];
+				const uint32_t nr = ce[C_NR], bv = ce[C_BV] & 0x7fffffffu;
 				if (bv != 0u && nr != 0u)
 					bv_eval(DescU{ hc + bv, hc }, H, g, k, p, x, hit, nxt, nmark, nleaf);
 				else

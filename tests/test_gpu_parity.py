@@ -292,3 +292,17 @@ def test_single_candidate_record_forms(built, gpu, four_terms):
     assert c.program_info()["cand1"] == 1
     c.close()
     both(prog, b, what=f"config4 four_terms={four_terms}")
+
+
+@pytest.mark.parametrize("engine", ["auto", "spec", "nojit", "linear", "nowide", "nocand1"])
+@pytest.mark.parametrize("name,make", [
+    ("nested256", lambda n: R.config3_nested(n)),
+    ("nested1024", lambda n: R.config3_nested(n, scale=4)),
+    ("classes9", lambda n: R.config3_classes(n))], ids=["nested256", "nested1024", "classes9"])
+def test_overlapping_acls(built, gpu, name, make, engine):
+    """Rule sets with overlapping keys (nested prefixes, wildcard ports: the
+    wide-bitmap and candidate-list engines) and with more key classes than a
+    block holds (a chain of blocks): first-match order as the oracle."""
+    b, prog = make(50_000)
+    got = both(prog, b, what=name, engine=engine)
+    assert summary(got)["enq"] > 0

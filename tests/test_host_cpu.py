@@ -213,16 +213,23 @@ def test_classify_without_gpu_fails_loudly(c):
 
 
 @pytest.mark.parametrize("cfg,flat,spec", [(2, True, True), (3, True, True), (4, True, True),
-                                           (5, False, True), ("classes", False, False)])
+                                           (5, False, True), ("classes", False, True),
+                                           ("noblock", False, False)])
 def test_specialised_kernel_compiles(built, cfg, flat, spec):
     """The embedded kernel sources compile with hipRTC (no GPU needed) into
     the program-specialised kernel of a program whose default CoS has a
-    classification block (flat programs and CoS trees such as config 5);
-    a default CoS on the linear scan (9 key classes) has none."""
+    classification block (flat programs, CoS trees such as config 5, a chain
+    of blocks for 9 key classes); a default CoS without rules has none."""
     L = cls.lib()
     L.mi_cls_spec_compile.restype = C.c_int
     L.mi_cls_spec_compile.argtypes = [C.c_void_p, C.c_size_t, C.c_int]
-    b, prog = R.config3_classes(100) if cfg == "classes" else R.CONFIGS[cfg](100)
+    if cfg == "classes":
+        b, prog = R.config3_classes(100)
+    elif cfg == "noblock":
+        b, prog = R.config2(100)
+        prog = [op for op in prog if op[0] != "pmr"]
+    else:
+        b, prog = R.CONFIGS[cfg](100)
     c = cls.Classifier(gpu=0)
     try:
         c.apply(prog)
@@ -230,5 +237,22 @@ def test_specialised_kernel_compiles(built, cfg, flat, spec):
         assert (c.program_info()["flat_engine"] >= 0) == flat
         for nw in ((4, 16) if cfg == 3 else (16,)):
             assert L.mi_cls_spec_compile(blob, len(blob), nw) == (0 if spec else 1)
+    finally:
+        c.close()
+
+
+def test_block_chain_for_many_classes(built):
+    """256 rules over 9 key classes: one block cannot hold them, so the
+    default CoS gets a chain of blocks (not the linear scan); 8 classes or
+    fewer keep a single block."""
+    c = cls.Classifier(gpu=0)
+    try:
+        c.apply(R.config3_classes(100)[1])
+        info = c.program_info()
+        assert info["chained"] == 1 and info["blocks"] == 1 and info["flat_engine"] == -1
+        c2 = cls.Classifier(gpu=0)
+        c2.apply(R.config3_nested(100)[1])
+        assert c2.program_info()["chained"] == 0
+        c2.close()
     finally:
         c.close()
