@@ -1742,14 +1742,23 @@ __device__ __forceinline__ void bv_eval(const D &blk, T H, bool act, const Pkt &
 		hit = h ? 1u : hit;
 		return;
 	}
-	uint32_t first = bv_first<FM>(blk, hb, H, act, k, p, x);
-	if constexpr (FM < 0 && !D::per_lane) {
-		for (uint32_t nx = hb(0) >> 8; nx != 0u;) {
-			const DescU nb{ blk.h + nx, blk.h };
-			const auto nh = nb.hdr();
-			first = min(first, bv_first<-1>(nb, nh, H, act, k, p, x));
-			nx = nh(0) >> 8;
+	uint32_t first;
+	if constexpr (FM < 0 && std::is_same<D, DescU>::value) {
+		// a chain (wave-uniform blocks only): one copy of the engines,
+		// looping over the blocks
+		first = BV_NONE;
+		DescU cur = blk;
+		DescV ch = hb;
+		for (;;) {
+			first = min(first, bv_first<-1>(cur, ch, H, act, k, p, x));
+			const uint32_t nx = ch(0) >> 8;
+			if (nx == 0u)
+				break;
+			cur = DescU{ blk.h + nx, blk.h };
+			ch = cur.hdr();
 		}
+	} else {
+		first = bv_first<FM>(blk, hb, H, act, k, p, x);
 	}
 	const bool h = act && first != BV_NONE;
 	const uint32_t rw2 = H[res + (h ? first : 0u)];
