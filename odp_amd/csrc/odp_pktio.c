@@ -1365,10 +1365,8 @@ static int pktio_recv(rt_pktio_t *e, odp_packet_t out[], int max_out)
 		 * so a packet allocation never fails on a staged frame (frames not
 		 * staged stay in the store for the next call; the reference instead
 		 * consumes the frame and stops on a failed allocation, pcap.c:324-327) */
-		rt_pool_t *pl = rt_pool(e->pool);
-
-		if (pl) {
-			long room = (long)pl->num_free - (p->pending ? (long)p->n : 0);
+		if (rt_pool(e->pool)) {
+			long room = (long)rt_pool_avail(e->pool) - (p->pending ? (long)p->n : 0);
 
 			if (room < (long)burst)
 				burst = room > 0 ? (uint32_t)room : 0u;

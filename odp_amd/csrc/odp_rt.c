@@ -56,6 +56,7 @@ static struct {
 	int sched_configured;
 } RT;
 
+static void pool_cache_flush(int idx);
 static __thread int tls_thr_id = -1;
 static __thread odp_thread_type_t tls_thr_type = ODP_THREAD_CONTROL;
 static __thread rt_queue_t *tls_atomic;     /* held atomic/ordered queue */
@@ -113,6 +114,8 @@ int odp_term_local(void)
 	if (tls_thr_id < 0)
 		return -1;
 	odp_schedule_release_atomic();
+	for (int i = 0; i < RT_MAX_POOLS; i++)
+		pool_cache_flush(i);
 	tls_thr_id = -1;
 	/* returns the number of threads still running (init.h) */
 	return __atomic_sub_fetch(&RT.thr_count, 1, __ATOMIC_RELAXED) > 0;
@@ -555,8 +558,11 @@ odp_pool_t odp_pool_create(const char *name, const odp_pool_param_t *param)
 	}
 	rt_pool_t *p = &RT.pool[idx];
 
+	static uint32_t pool_gen;
+
 	memset(p, 0, sizeof(*p));
 	p->used = 1;
+	p->gen = ++pool_gen;
 	odp_spinlock_unlock(&RT.lock);
 
 	void *mem = NULL;
@@ -602,6 +608,7 @@ int odp_pool_destroy(odp_pool_t h)
 
 	if (!p)
 		return -1;
+	pool_cache_flush((int)(p - RT.pool));
 	if (p->num_free != p->num)
 		RT_ERR("pool %s destroyed with %u events in use\n", p->name, p->num - p->num_free);
 	free(p->mem);
@@ -679,7 +686,7 @@ uint64_t odp_pool_to_u64(odp_pool_t h) { return (uint64_t)(uintptr_t)h; }
 int odp_pool_index(odp_pool_t h) { return rt_pool(h) ? (int)((uintptr_t)h - 1) : -1; }
 unsigned int odp_pool_max_index(void) { return RT_MAX_POOLS - 1; }
 
-static int pool_alloc(rt_pool_t *p, ev_hdr_t *out[], int num)
+static int pool_take(rt_pool_t *p, ev_hdr_t *out[], int num)
 {
 	int n = 0;
 
@@ -693,15 +700,114 @@ static int pool_alloc(rt_pool_t *p, ev_hdr_t *out[], int num)
 	return n;
 }
 
+static void pool_give(rt_pool_t *p, ev_hdr_t *const e[], int num)
+{
+	if (num <= 0)
+		return;
+	for (int i = 0; i + 1 < num; i++)
+		e[i]->next = e[i + 1];
+	odp_spinlock_lock(&p->lock);
+	e[num - 1]->next = p->free_list;
+	p->free_list = e[0];
+	p->num_free += (uint32_t)num;
+	odp_spinlock_unlock(&p->lock);
+}
+
+/* Per-thread cache of free events in front of a large pool's locked free
+ * list (as a DPDK mempool cache): allocations and frees take the pool lock
+ * once per PC_BATCH events instead of per event.  Pools below PC_MIN_POOL
+ * events are not cached (a thread's cache would hold a noticeable share of
+ * them away from the others).  Entries are tagged with the pool's creation
+ * number; odp_term_local() and odp_pool_destroy() return the calling
+ * thread's cached events. */
+#define PC_SIZE 512
+#define PC_BATCH 256
+#define PC_MIN_POOL 4096u
+typedef struct {
+	uint32_t gen;
+	int n;
+	ev_hdr_t *e[PC_SIZE];
+} pool_cache_t;
+static __thread pool_cache_t *tls_pc[RT_MAX_POOLS];
+
+static pool_cache_t *pool_cache(rt_pool_t *p)
+{
+	const int idx = (int)(p - RT.pool);
+	pool_cache_t *c = tls_pc[idx];
+
+	if (p->num < PC_MIN_POOL)
+		return NULL;
+	if (!c) {
+		c = calloc(1, sizeof(*c));
+		if (!c)
+			return NULL;
+		c->gen = p->gen;
+		tls_pc[idx] = c;
+	}
+	if (c->gen != p->gen) {   /* cache of a destroyed pool in this slot */
+		c->n = 0;
+		c->gen = p->gen;
+	}
+	return c;
+}
+
+static void pool_cache_flush(int idx)
+{
+	pool_cache_t *c = tls_pc[idx];
+
+	if (c && c->n && RT.pool[idx].used && c->gen == RT.pool[idx].gen)
+		pool_give(&RT.pool[idx], c->e, c->n);
+	if (c)
+		c->n = 0;
+}
+
+uint32_t rt_pool_avail(odp_pool_t h)
+{
+	rt_pool_t *p = rt_pool(h);
+
+	if (!p)
+		return 0;
+	const pool_cache_t *c = tls_pc[p - RT.pool];
+
+	return p->num_free + (c && c->gen == p->gen ? (uint32_t)c->n : 0u);
+}
+
+static int pool_alloc(rt_pool_t *p, ev_hdr_t *out[], int num)
+{
+	pool_cache_t *c = pool_cache(p);
+	int n = 0;
+
+	if (!c)
+		return pool_take(p, out, num);
+	while (n < num) {
+		if (c->n == 0) {
+			c->n = pool_take(p, c->e, PC_BATCH);
+			if (c->n == 0)
+				break;
+		}
+		int take = num - n < c->n ? num - n : c->n;
+
+		memcpy(out + n, c->e + c->n - take, (size_t)take * sizeof(ev_hdr_t *));
+		c->n -= take;
+		n += take;
+	}
+	return n;
+}
+
 static void pool_free(ev_hdr_t *e)
 {
 	rt_pool_t *p = &RT.pool[e->pool];
+	pool_cache_t *c = pool_cache(p);
 
-	odp_spinlock_lock(&p->lock);
-	e->next = p->free_list;
-	p->free_list = e;
-	p->num_free++;
-	odp_spinlock_unlock(&p->lock);
+	if (!c) {
+		pool_give(p, &e, 1);
+		return;
+	}
+	if (c->n == PC_SIZE) {
+		pool_give(p, c->e + PC_SIZE - PC_BATCH, PC_BATCH);
+		c->n -= PC_BATCH;
+	}
+	c->e[c->n++] = e;
 }
 
 /* ================================================================ packets */

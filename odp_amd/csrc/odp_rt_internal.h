@@ -67,7 +67,8 @@ typedef struct rt_pool {
 	uint32_t num;
 	uint32_t data_cap;      /* packet data capacity (excl. head/tailroom) */
 	ev_hdr_t *free_list;
-	uint32_t num_free;
+	uint32_t num_free;      /* on free_list (thread caches not counted) */
+	uint32_t gen;           /* creation number: tags the thread caches */
 	odp_spinlock_t lock;
 } rt_pool_t;
 
@@ -98,6 +99,9 @@ struct rt_queue {
 /* runtime-private entry points */
 pkt_hdr_t *rt_pkt_hdr(odp_packet_t pkt);
 rt_pool_t *rt_pool(odp_pool_t pool);
+/* free events of a pool this thread can allocate: its free list plus the
+ * calling thread's cache */
+uint32_t rt_pool_avail(odp_pool_t pool);
 int rt_queue_enq_multi(rt_queue_t *q, const odp_event_t ev[], int num);
 int rt_queue_deq_multi_raw(rt_queue_t *q, odp_event_t ev[], int num);
 int rt_thread_id(void);
