@@ -50,6 +50,14 @@ WORKLOAD = {2: "config2", 3: "config3", 4: "config4", 5: "config5", 33: "config3
             38: "config3_9classes"}
 
 
+_T0 = time.perf_counter()
+
+
+def log(msg):
+    """Progress on stderr (a long run keeps writing, so it is not taken to be hung)."""
+    print(f"[bench {time.perf_counter() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
 def parse_args():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -364,6 +372,7 @@ def bench_cfg(cls, cfg, a, dev, local, steps, warmup, pktin_opt=0, parity=True, 
     its records against the oracle."""
     import numpy as np
     from odp_amd import pktgen as pg, rules as R
+    log(f"extra {WORKLOAD[cfg]}{' pktin_opt' if pktin_opt else ''}: workload")
     b2, p2 = make_workload(cfg, a.n, 0)
     if pktin_opt:
         pg.set_checksums(b2)
@@ -371,7 +380,9 @@ def bench_cfg(cls, cfg, a, dev, local, steps, warmup, pktin_opt=0, parity=True, 
     c2.apply(p2)
     if pktin_opt:
         c2.set_pktin_opt(pktin_opt)
+    log("  rules loaded, waiting for the specialised kernel")
     spec = c2.spec_wait() == 0 and not pktin_opt
+    log(f"  specialised={spec}, timing")
     info = c2.program_info()
     engine = ("linear scan" if info["blocks"] == 0 else
               ["direct", "candidate lists", "bitmap", "wide bitmap", "single candidate"][
@@ -395,6 +406,7 @@ def bench_cfg(cls, cfg, a, dev, local, steps, warmup, pktin_opt=0, parity=True, 
     if pmc:
         e["issue"] = issue_roof(k1, pmc)
     if parity:
+        log("  oracle parity")
         o_prog = p2
         if pktin_opt:
             from oracle.oracle import Oracle
@@ -474,7 +486,9 @@ def main():
             node_lens = np.full(a.n * world, 60)
         bnd = cls.shard(node_lens.astype(np.uint16), world)
         n_rank = int(bnd[rank + 1] - bnd[rank])
+    log(f"workload {WORKLOAD[a.config]}: {n_rank} packets")
     batch, prog = make_workload(a.config, n_rank, rank)
+    log("rules")
     c = cls.Classifier(gpu=local)
     c.apply(prog)
     if a.pktin_opt:
@@ -484,6 +498,7 @@ def main():
     # rule load is control plane: the program-specialised kernel (compiled in
     # the background after the rules are loaded) is ready before timing
     spec = c.spec_wait() == 0
+    log(f"specialised={spec}, timing")
 
     wall, kms, t_out = time_device(c, batch, dev, a.steps, a.warmup, dist_on, a.rotate,
                                    a.streams)
@@ -538,6 +553,7 @@ def main():
         }
         if not a.no_parity and not a.timed_only:
             # this rank's records, every one bit-exact vs the oracle
+            log("oracle parity")
             line["parity_vs_oracle"] = oracle_parity(prog, batch, out, pktin_opt=a.pktin_opt)
         if world == 1 and not a.timed_only:
             if pmc:
@@ -545,15 +561,18 @@ def main():
             w2, _, _ = time_device(c, batch, dev, a.steps, a.warmup, rotate=a.rotate, streams=2)
             line["pipelined"] = {"streams": 2, "mpkts_per_s": round(batch.n * a.steps / w2 / 1e6, 2),
                                  "ms_per_step": round(w2 / a.steps * 1e3, 5)}
+            log("e2e")
             try:
                 line["e2e"] = time_e2e(c, batch, dev)
             except Exception as e:   # recorded, never fatal
                 line["e2e"] = {"error": str(e)}
+            log("ODP runtime receive rate")
             try:
                 line["e2e"]["runtime"] = time_runtime(batch, prog)
             except Exception as e:   # recorded, never fatal
                 line["e2e"]["runtime"] = {"error": str(e)}
             if not a.no_cpu:
+                log("cpu baseline")
                 line["cpu_baseline"] = cpu_baseline(prog, batch, a.cpu_seconds)
             if not a.no_extra:
                 extra = {}

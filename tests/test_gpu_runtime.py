@@ -240,8 +240,9 @@ def test_rx_cos_destroyed_while_burst_in_flight(built, gpu, tmp_path):
     odp_pktin_recv calls while the first call's burst is still in flight on
     the GPU.  That burst was classified under the old rule snapshot; it must
     be delivered under the current one (as the synchronous path would), not
-    to the destroyed CoS's queues: every packet reaches the new CoS, none is
-    discarded."""
+    to the destroyed CoS's queues: every packet the current rules enqueue
+    reaches the new CoS, and in_discards counts only the frames the oracle
+    discards (compare() checks the pktio counters)."""
     frames = H.pcap_frames([f for _, f in zoo.all_frames()])
     pc = str(tmp_path / "in.pcap")
     H.write_pcap(pc, frames)
@@ -257,4 +258,4 @@ def test_rx_cos_destroyed_while_burst_in_flight(built, gpu, tmp_path):
                        env={"ODP_AMD_RX_BURST": "16", "RX_SWITCH_RULES": r2})
     exp = H.expected(before + after, frames * 2, 1, 1, 4)
     H.compare(got, exp)
-    assert got[1][2] == 0, got[1]   # in_discards
+    assert got[0].get("B"), "nothing reached the new default CoS"
