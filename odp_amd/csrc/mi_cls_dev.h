@@ -1502,11 +1502,12 @@ __device__ __forceinline__ bool split_key(const D &blk, uint32_t ro, bool act, c
 
 // First holding rule of one non-direct block (modes 1-4) for the lanes in
 // `act` (BV_NONE: none); rule numbers index the block's result words.
-template <int FM, typename D, typename T>
+template <int FM, bool CHAIN, typename D, typename T>
 __device__ __forceinline__ uint32_t bv_first(const D &blk, const DescV &hb, T H, bool act,
 					     const Pkt &k, const Parsed &p, const Fields &x)
 {
-	const uint32_t mode = FM >= 0 ? (uint32_t)FM : (hb(0) & 0xffu), ncls = hb(1);
+	// header word 0: mode | next block of a chain << 8 (CHAIN kernels only)
+	const uint32_t mode = FM >= 0 ? (uint32_t)FM : (CHAIN ? (hb(0) & 0xffu) : hb(0)), ncls = hb(1);
 	uint32_t first = BV_NONE;
 	if (mode == 2u) {
 		// bitmap: AND of the classes' 32-bit rows and the alive row
@@ -1717,14 +1718,18 @@ __device__ __forceinline__ uint32_t bv_first(const D &blk, const DescV &hb, T H,
 // rules with at most BV_MAX_CLS classes and the CoS's rule numbering; the
 // first holding rule is the smallest over the chain.  Chained CoS are
 // evaluated wave-uniformly only (their CoS entry's block word has bit 31
-// set, which the per-lane rounds treat as "no block").
-template <int FM = -1, typename D, typename T>
+// set), and only by kernels built with CHAIN (the generic kernels of
+// programs without CoS trees): the chain loop's live state pushed the tree
+// kernels (DIV) into VGPR spills (config5 46.7 -> 51.2 us, 28 B scratch per
+// lane), so the host builds no chains for tree programs -- their CoS with
+// more key classes than a block holds take the linear scan.
+template <int FM = -1, bool CHAIN = false, typename D, typename T>
 __device__ __forceinline__ void bv_eval(const D &blk, T H, bool act, const Pkt &k, const Parsed &p,
 					const Fields &x, uint32_t &hit, uint32_t &nxt, uint32_t &nmark,
 					uint32_t &nleaf)
 {
 	const auto hb = blk.hdr();   // the block header (words 0-7)
-	const uint32_t mode = FM >= 0 ? (uint32_t)FM : (hb(0) & 0xffu), res = hb(2);
+	const uint32_t mode = FM >= 0 ? (uint32_t)FM : (CHAIN ? (hb(0) & 0xffu) : hb(0)), res = hb(2);
 	if (mode == 0u) {
 		// direct: one class, the slot holds the result word of the first
 		// live rule of its key (BV_EMPTY: none); a miss takes the block's
@@ -1743,14 +1748,14 @@ __device__ __forceinline__ void bv_eval(const D &blk, T H, bool act, const Pkt &
 		return;
 	}
 	uint32_t first;
-	if constexpr (FM < 0 && std::is_same<D, DescU>::value) {
+	if constexpr (CHAIN && FM < 0 && std::is_same<D, DescU>::value) {
 		// a chain (wave-uniform blocks only): one copy of the engines,
 		// looping over the blocks
 		first = BV_NONE;
 		DescU cur = blk;
 		DescV ch = hb;
 		for (;;) {
-			first = min(first, bv_first<-1>(cur, ch, H, act, k, p, x));
+			first = min(first, bv_first<-1, true>(cur, ch, H, act, k, p, x));
 			const uint32_t nx = ch(0) >> 8;
 			if (nx == 0u)
 				break;
@@ -1758,7 +1763,7 @@ __device__ __forceinline__ void bv_eval(const D &blk, T H, bool act, const Pkt &
 			ch = cur.hdr();
 		}
 	} else {
-		first = bv_first<FM>(blk, hb, H, act, k, p, x);
+		first = bv_first<FM, CHAIN>(blk, hb, H, act, k, p, x);
 	}
 	const bool h = act && first != BV_NONE;
 	const uint32_t rw2 = H[res + (h ? first : 0u)];
@@ -2046,7 +2051,8 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 	// the default CoS's words (the first descent round always evaluates it)
 	const cword_t dce = hc + COS_WORDS * (uint32_t)max(def_cos, 0);
 	const uint32_t d_nr = def_cos >= 0 ? dce[C_NR] : 0u;
-	const uint32_t d_bv = dce[C_BV] & 0x7fffffffu, d_rec0 = dce[C_REC0];   // bit 31: chained
+	// bit 31: a chain of blocks (never set in tree programs)
+	const uint32_t d_bv = DIV ? dce[C_BV] : dce[C_BV] & 0x7fffffffu, d_rec0 = dce[C_REC0];
 	const bool stats_on = a.stats != nullptr;
 	typedef typename std::conditional<LT, lword_t, gword_t>::type hot_t;
 	hot_t H;
@@ -2309,7 +2315,8 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 				bv_eval<FM>(DescU{ hc + d_bv, hc }, H, g, k, p, x, hit, nxt, nmark, nleaf);
 			} else {
 				if (d_bv != 0u && d_nr != 0u)
-					bv_eval(DescU{ hc + d_bv, hc }, H, g, k, p, x, hit, nxt, nmark, nleaf);
+					bv_eval<-1, !DIV>(DescU{ hc + d_bv, hc }, H, g, k, p, x, hit, nxt, nmark,
+							  nleaf);
 				else
 					linear_scan(prog, d_rec0, d_nr, g, k, p, x, hit, nxt, nmark);
 			}
@@ -2328,8 +2335,7 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 					const uint32_t my_nr = H[ci + C_NR];
 					const uint32_t my_bv = H[ci + C_BV];
 					const bool empty = pend != 0u && my_nr == 0u;
-					// chained blocks (bit 31) are evaluated wave-uniformly below
-					const bool bvl = pend != 0u && my_nr != 0u && my_bv != 0u && (my_bv >> 31) == 0u;
+					const bool bvl = pend != 0u && my_nr != 0u && my_bv != 0u;
 					if (__ballot(bvl))
 						bv_eval(DescL<hot_t>{ H, my_bv, hc }, H, bvl, k, p, x, hit, nxt, nmark,
 							nleaf);
@@ -2344,9 +2350,10 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 				const bool g = act && cur == c1;
 				grp = g ? 1u : 0u;
 				const cword_t ce = hc + COS_WORDS * (uint32_t)c1;
-				const uint32_t nr = ce[C_NR], bv = ce[C_BV] & 0x7fffffffu;
+				const uint32_t nr = ce[C_NR], bv = DIV ? ce[C_BV] : ce[C_BV] & 0x7fffffffu;
 				if (bv != 0u && nr != 0u)
-					bv_eval(DescU{ hc + bv, hc }, H, g, k, p, x, hit, nxt, nmark, nleaf);
+					bv_eval<-1, !DIV>(DescU{ hc + bv, hc }, H, g, k, p, x, hit, nxt, nmark,
+							  nleaf);
 				else
 					linear_scan(prog, ce[C_REC0], nr, g, k, p, x, hit, nxt, nmark);
 			}

@@ -354,6 +354,7 @@ int main(int argc, char *argv[])
 	count_only = getenv("RX_COUNT_ONLY") != NULL;
 	if (odp_pktio_start(pktio))
 		return 8;
+	fprintf(stderr, "T started\n");
 	/* rate runs time the steady state: GPU context, rule upload and the
 	 * warm-up launch happen in odp_pktio_start */
 	odp_time_t t_start = odp_time_local();
@@ -481,7 +482,10 @@ int main(int argc, char *argv[])
 				       qs_.discards);
 		}
 	}
+	fprintf(stderr, "T loop done %.1f ms\n", odp_time_diff_ns(odp_time_local(), t_start) / 1e6);
 	odp_pktio_stop(pktio);
+	fprintf(stderr, "T stopped %.1f ms\n", odp_time_diff_ns(odp_time_local(), t_start) / 1e6);
 	odp_pktio_close(pktio);
+	fprintf(stderr, "T closed %.1f ms\n", odp_time_diff_ns(odp_time_local(), t_start) / 1e6);
 	return 0;
 }

@@ -84,8 +84,16 @@ def run_driver(pktio, rules_path, mode="sched", layer=4, cos_pools=1, cls=1, src
         args.append(src)
     e = dict(os.environ)
     e.update(env or {})
-    r = subprocess.run(args, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
-                       timeout=timeout, env=e)
+    try:
+        r = subprocess.run(args, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                           timeout=timeout, env=e)
+    except subprocess.TimeoutExpired as t:
+        # the driver's phase markers (stderr "T ...") and its last output say
+        # where it stopped
+        err = (t.stderr or b"")[-2000:]
+        out = (t.stdout or b"")[-600:]
+        raise AssertionError(f"rx_driver timed out after {timeout} s: {' '.join(args)}\n"
+                             f"stderr tail: {err!r}\nstdout tail: {out!r}") from None
     assert r.returncode == 0, f"rx_driver rc={r.returncode}\n{r.stderr[-2000:]}"
     queues = defaultdict(list)
     stats = None

@@ -306,3 +306,40 @@ def test_overlapping_acls(built, gpu, name, make, engine):
     b, prog = make(50_000)
     got = both(prog, b, what=name, engine=engine)
     assert summary(got)["enq"] > 0
+
+
+def _under_root(prog, root_first=False):
+    """The program one level down: a new root CoS becomes the default, its one
+    rule (IPv4 ethertype) leads to the old default CoS -- a CoS tree whose
+    second level holds the program's rules.  root_first: the root CoS's rule
+    set also gets the program's rules (a tree whose default CoS has more key
+    classes than a block holds)."""
+    n = R.cos_count(prog)
+    old = next(op[1] for op in prog if op[0] == "default")
+    out = [op for op in prog if op[0] == "cos"] + [R.cos("root", queue=9), ("default", n)]
+    out.append(("pmr", [R.t_be16(R.PMR_ETHTYPE_0, 0x0800)], n, old, 0))
+    for op in prog:
+        if op[0] == "pmr":
+            out.append(op)
+            if root_first and op[2] == old:
+                out.append(("pmr", op[1], n, op[3], op[4]))
+    return out
+
+
+@pytest.mark.parametrize("root_first", [False, True], ids=["second_level", "default_cos"])
+@pytest.mark.parametrize("engine", ["auto", "linear"])
+def test_many_classes_in_tree(built, gpu, root_first, engine):
+    """A CoS tree with a CoS whose rules span 9 key classes: tree programs
+    build no chains of blocks (the tree kernels scan such a CoS linearly);
+    first-match order and marks as the oracle, at the second level and on
+    the default CoS."""
+    from odp_amd.cls import Classifier
+    b, prog = R.config3_classes(40_000)
+    tprog = _under_root(prog, root_first)
+    c = Classifier(gpu=0)
+    c.apply(tprog)
+    info = c.program_info()
+    c.close()
+    assert info["tree"] and info["chained"] == 0
+    got = both(tprog, b, what=f"classes9 tree root_first={root_first}", engine=engine)
+    assert summary(got)["enq"] > 0

@@ -256,5 +256,13 @@ def test_block_chain_for_many_classes(built):
         c2.apply(R.config3_nested(100)[1])
         assert c2.program_info()["chained"] == 0
         c2.close()
+        # the same rules in a CoS tree: the tree kernels scan them linearly
+        from tests.test_gpu_parity import _under_root
+        for root_first in (False, True):
+            c3 = cls.Classifier(gpu=0)
+            c3.apply(_under_root(R.config3_classes(100)[1], root_first))
+            i3 = c3.program_info()
+            c3.close()
+            assert i3["tree"] and i3["chained"] == 0, i3
     finally:
         c.close()
