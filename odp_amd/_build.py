@@ -1,6 +1,8 @@
 """Native build of the MI355X classification path (in-tree, no JIT cache).
 
   odp_amd/libmi_cls.so   hipcc --offload-arch=gfx950: HIP kernels + mi_cls.h C ABI
+  odp_amd/mi_cls_jitc    g++ over hipRTC: compiles program-specialised kernels,
+                         started by libmi_cls.so as a child process
   odp_amd/libodp_cls.so  gcc: the ODP library of this build -- classification
                          control plane (odp_cls_api.h) + runtime subset and
                          packet I/O (odp_rt.h), linked against libmi_cls.so
@@ -81,10 +83,17 @@ def build(force: bool = False, out_dir: str = PKG, defines=()) -> list[str]:
             jobs.append([HIPCC] + flags + stub + ["-c", "-o", obj, src])
         with cf.ThreadPoolExecutor(max_workers=len(jobs)) as ex:
             list(ex.map(_run, jobs))
-        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", mi_so] + objs +
-             ["-lhiprtc"])
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", mi_so] + objs)
         shutil.rmtree(tmp, ignore_errors=True)
         built.append(mi_so)
+    # the program-specialised kernels' compiler, run as a child process of
+    # libmi_cls.so (mi_cls.hip spec_compile): host code over hipRTC
+    jitc_src = os.path.join(SRC, "mi_cls_jitc.cpp")
+    jitc = os.path.join(out_dir, "mi_cls_jitc")
+    if force or _stale(jitc, [jitc_src]):
+        _run(["g++", "-O2", "-std=c++17", "-Wall", "-D__HIP_PLATFORM_AMD__", "-I", "/opt/rocm/include",
+              "-o", jitc, jitc_src, "-L", "/opt/rocm/lib", "-lhiprtc", "-Wl,-rpath,/opt/rocm/lib"])
+        built.append(jitc)
     if force or _stale(odp_so, odp_srcs + [mi_so] + rt_hdrs):
         _run(["gcc", "-O2", "-std=gnu11", "-Wall", "-Wextra", "-fPIC", "-shared", "-I", INC,
               "-o", odp_so] + odp_srcs + ["-L", out_dir, "-lmi_cls", "-Wl,-rpath,$ORIGIN",

@@ -69,6 +69,8 @@ typedef struct {
 	uint16_t *slen;
 	mi_cls_result_t *res;
 	odp_packet_t *pk;       /* loop driver: the packets themselves */
+	odp_packet_t *tmp;      /* delivery: packets grouped by queue */
+	uint32_t tmp_cap;
 	uint32_t n_cap;
 	int arr_pinned;
 	int n;
@@ -843,6 +845,9 @@ static void rx_set_arrays_free(rx_set_t *s)
 	hmem_free(s->slen, s->arr_pinned);
 	hmem_free(s->res, s->arr_pinned);
 	free(s->pk);
+	free(s->tmp);
+	s->tmp = NULL;
+	s->tmp_cap = 0;
 	s->soff = NULL;
 	s->slen = NULL;
 	s->res = NULL;
@@ -1193,6 +1198,241 @@ static int rx_classify(rt_pktio_t *e, rx_set_t *s, int pipe)
 	return 0;
 }
 
+/* Per-chunk pktio counters of a delivery. */
+typedef struct {
+	uint64_t in_errors, in_discards, octets, packets;
+} rx_cnt_t;
+
+/* The host steps of loopback_recv / pcapif_recv_pkt for frames [lo, hi) of
+ * set s (loop.c:253-384, pcap.c:299-352; _odp_packet_parse_common's result
+ * applied at the pktio's layer, _odp_cls_classify_packet's outcome, the
+ * packet in its final pool, _odp_pktio_packet_to_pool): s->pk[i] becomes the
+ * packet to deliver, or ODP_PACKET_INVALID.  (Preparing chunks of a burst on
+ * helper threads measured slower -- 14.3 -> 6.4 Mpkt/s with four helpers,
+ * profiles/r03g_rx_helpers_ab.txt: each packet's header line then moves between cores
+ * on its way to the queue and the consumer -- so one thread does it.) */
+static void rx_prepare(rt_pktio_t *e, rx_set_t *s, int lo, int hi, rx_cnt_t *c)
+{
+	const odp_proto_layer_t layer = e->parse_layer;
+
+	for (int i = lo; i < hi; i++) {
+		mi_cls_result_t r;
+		odp_packet_t pkt = e->drv == DRV_LOOP ? s->pk[i] : ODP_PACKET_INVALID;
+		uint32_t len = s->slen[i];
+
+		s->pk[i] = ODP_PACKET_INVALID;
+		if (i + 8 < hi) {   /* frames read in place are cold in the CPU caches */
+			const uint8_t *nf = s->base + s->soff[i + 8];
+			const uint32_t nl = s->slen[i + 8];
+
+			for (uint32_t b = 0; b < nl; b += 64)
+				__builtin_prefetch(nf + b);
+		}
+		if (layer != ODP_PROTO_LAYER_NONE) {
+			r = s->res[i];
+			apply_layer(&r, layer);
+			if (r.err || r.outcome == MI_CLS_OUT_PARSE_DROP)
+				c->in_errors++;
+			if (r.outcome == MI_CLS_OUT_PARSE_DROP) {
+				odp_packet_free(pkt);
+				continue;
+			}
+		} else {
+			memset(&r, 0, sizeof(r));
+			r.cos = 0xff;
+		}
+		odp_pool_t pool = e->pool;
+
+		if (e->cls_enabled) {
+			if (r.outcome == MI_CLS_OUT_DISCARD || r.outcome == MI_CLS_OUT_LOOP)
+				c->in_discards++;
+			if (r.outcome != MI_CLS_OUT_ENQ) {
+				odp_packet_free(pkt);
+				continue;
+			}
+			odp_pool_t cp = odp_amd_cls_pool_of(r.cos);
+
+			if (cp != ODP_POOL_INVALID)
+				pool = cp;
+		}
+		/* packet in the final pool (_odp_pktio_packet_to_pool) */
+		if (pkt == ODP_PACKET_INVALID) {
+			pkt = odp_packet_alloc(pool, len);
+			if (pkt == ODP_PACKET_INVALID) {
+				if (e->cls_enabled)
+					c->in_discards++;
+				continue;
+			}
+			memcpy(odp_packet_data(pkt), s->base + s->soff[i], len);
+		} else if (odp_packet_pool(pkt) != pool) {
+			odp_packet_t np = odp_packet_alloc(pool, len);
+
+			if (np == ODP_PACKET_INVALID) {
+				odp_packet_free(pkt);
+				c->in_discards++;
+				continue;
+			}
+			pkt_hdr_t *sh = rt_pkt_hdr(pkt);
+
+			memcpy(odp_packet_data(np), sh->head + sh->data_off, len);
+			rt_pkt_hdr(np)->user_ptr = sh->user_ptr;
+			odp_packet_free(pkt);
+			pkt = np;
+		}
+		pkt_hdr_t *h = rt_pkt_hdr(pkt);
+
+		if (layer != ODP_PROTO_LAYER_NONE) {
+			h->in_flags = r.in_flags;
+			h->err = r.err;
+			h->l2 = 0;
+			h->l3 = r.l3_offset;
+			h->l4 = r.l4_offset;
+		} else {
+			h->in_flags = 0;
+			h->err = 0;
+		}
+		h->input = e->hdl;
+		if (!h->err) {
+			c->octets += len;
+			c->packets++;
+		}
+		if (e->cls_enabled) {
+			h->cos = r.cos;
+			h->cls_mark = r.mark;
+			h->dst_queue = odp_amd_cls_queue_of(r.cos, r.queue);
+		}
+		s->pk[i] = pkt;
+	}
+}
+
+/* Enqueue the delivered packets pk[0..n) in arrival order.  _odp_cls_enq
+ * (odp_classification_internal.h:171-201) enqueues runs of equal
+ * (dst_queue, CoS); when every run of the burst takes the plain enqueue (no
+ * packet vectors, no aggregator), the runs of one queue are joined into one
+ * enqueue call per queue instead -- each queue still receives its packets in
+ * arrival order, and nothing outside the burst can tell the two apart (the
+ * whole burst is enqueued before the receive call returns).  Per-CoS queue
+ * statistics are kept as per run.  Runs of CoS with packet vectors or
+ * aggregators keep the reference's per-run form (their vector boundaries
+ * depend on it). */
+#define RX_GROUP_MAXQ 64
+#define RX_GROUP_HASH 256      /* open-addressing slots: queue -> group */
+static inline uint32_t rx_qhash(odp_queue_t q)
+{
+	const uint64_t x = (uint64_t)(uintptr_t)q * 0x9E3779B97F4A7C15ull;
+
+	return (uint32_t)(x >> 56);   /* 8 bits: RX_GROUP_HASH slots */
+}
+
+static void rx_enqueue(odp_packet_t pk[], int n, odp_packet_t *tmp, uint8_t *gidx)
+{
+	struct {
+		odp_queue_t q;
+		int cnt, fill;
+	} g[RX_GROUP_MAXQ];
+	int ng = 0, plain = 1;
+	int8_t mode_of_cos[256];   /* 1 plain, 0 not, -1 unknown */
+	uint8_t slot_grp[RX_GROUP_HASH];   /* group + 1, 0 empty */
+
+	memset(mode_of_cos, -1, sizeof(mode_of_cos));
+	memset(slot_grp, 0, sizeof(slot_grp));
+	for (int i = 0; i < n; i++) {
+		pkt_hdr_t *h = rt_pkt_hdr(pk[i]);
+		const uint32_t cos = h->cos & 0xffu;
+
+		if (mode_of_cos[cos] < 0) {
+			odp_pool_t vp = ODP_POOL_INVALID;
+			uint32_t vmax = 0;
+			int aggr = 0;
+			const int std = odp_amd_cls_cos_enq_mode(cos, &vp, &vmax, &aggr);
+
+			mode_of_cos[cos] = std > 0 && !aggr;
+		}
+		if (!mode_of_cos[cos]) {
+			plain = 0;
+			break;
+		}
+		uint32_t sl = rx_qhash(h->dst_queue);
+
+		while (slot_grp[sl] && g[slot_grp[sl] - 1].q != h->dst_queue)
+			sl = (sl + 1) & (RX_GROUP_HASH - 1);
+		if (!slot_grp[sl]) {
+			if (ng == RX_GROUP_MAXQ) {
+				plain = 0;
+				break;
+			}
+			g[ng].q = h->dst_queue;
+			g[ng].cnt = 0;
+			slot_grp[sl] = (uint8_t)++ng;
+		}
+		gidx[i] = (uint8_t)(slot_grp[sl] - 1);
+		g[slot_grp[sl] - 1].cnt++;
+	}
+	if (!plain) {
+		/* the reference's form: one enqueue per run */
+		int nrun = 0;
+
+		for (int i = 0; i < n; i++) {
+			if (nrun) {
+				pkt_hdr_t *ph = rt_pkt_hdr(pk[i - 1]), *h = rt_pkt_hdr(pk[i]);
+
+				if (ph->dst_queue != h->dst_queue || ph->cos != h->cos) {
+					cos_enq_run(&pk[i - nrun], nrun);
+					nrun = 0;
+				}
+			}
+			nrun++;
+		}
+		if (nrun)
+			cos_enq_run(&pk[n - nrun], nrun);
+		return;
+	}
+	/* counting sort by queue, stable: each group's packets in arrival order */
+	int at = 0;
+
+	for (int k = 0; k < ng; k++) {
+		g[k].fill = at;
+		at += g[k].cnt;
+	}
+	for (int i = 0; i < n; i++)
+		tmp[g[gidx[i]].fill++] = pk[i];
+	at = 0;
+	for (int k = 0; k < ng; k++) {
+		odp_packet_t *gp = tmp + at;
+		const int num = g[k].cnt;
+		int r = odp_queue_enq_multi(g[k].q, (const odp_event_t *)(void *)gp, num);
+
+		at += num;
+		if (r < 0)
+			r = 0;
+		if (r != num)
+			odp_packet_free_multi(&gp[r], num - r);
+		/* queue statistics as per run of the reference: per CoS of the queue */
+		int done = 0;
+
+		for (int j = 0; j < num && done < num; j++) {
+			const uint32_t cos = rt_pkt_hdr(gp[j])->cos;
+			int first = 1;
+
+			for (int t = 0; t < j && first; t++)
+				first = rt_pkt_hdr(gp[t])->cos != cos;
+			if (!first)
+				continue;
+			uint64_t ok = 0, bad = 0;
+
+			for (int t = j; t < num; t++)
+				if (rt_pkt_hdr(gp[t])->cos == cos) {
+					if (t < r)
+						ok++;
+					else
+						bad++;
+				}
+			done += (int)(ok + bad);
+			odp_amd_cls_queue_stats_add(cos, cos_slot_of(cos, g[k].q), ok, bad);
+		}
+	}
+}
+
 /* Wait for set s's records and deliver its packets: classified ones to their
  * CoS queues, the rest (classifier disabled) into out[] (at most max_out).
  * Returns the packets placed in out[]. */
@@ -1228,116 +1468,44 @@ static int rx_finish(rt_pktio_t *e, rx_set_t *s, odp_packet_t out[], int max_out
 
 	e->prof[1] += t2 - t1;
 	s->pending = 0;
-	odp_packet_t *run = s->pk;   /* reused in place: run[j] <= pk[i], j <= i */
-	int nrun = 0, num_rx = 0;
-	uint64_t octets = 0, packets = 0;
+	rx_cnt_t c;
 
-	for (int i = 0; i < s->n; i++) {
-		mi_cls_result_t r;
-		odp_packet_t pkt = e->drv == DRV_LOOP ? s->pk[i] : ODP_PACKET_INVALID;
-		uint32_t len = s->slen[i];
+	memset(&c, 0, sizeof(c));
+	rx_prepare(e, s, 0, s->n, &c);
+	/* the delivered packets, compacted in arrival order */
+	int nd = 0, num_rx = 0;
 
-		if (i + 8 < s->n) {   /* frames read in place are cold in the CPU caches */
-			const uint8_t *nf = s->base + s->soff[i + 8];
-			const uint32_t nl = s->slen[i + 8];
-
-			for (uint32_t b = 0; b < nl; b += 64)
-				__builtin_prefetch(nf + b);
+	for (int i = 0; i < s->n; i++)
+		if (s->pk[i] != ODP_PACKET_INVALID)
+			s->pk[nd++] = s->pk[i];
+	if (e->cls_enabled) {
+		if (!s->tmp || s->tmp_cap < s->n_cap) {
+			/* grouped packets, then one group index byte per packet */
+			free(s->tmp);
+			s->tmp = malloc(s->n_cap * (sizeof(odp_packet_t) + 1u));
+			s->tmp_cap = s->tmp ? s->n_cap : 0;
 		}
-
-		if (layer != ODP_PROTO_LAYER_NONE) {
-			r = s->res[i];
-			apply_layer(&r, layer);
-			if (r.err || r.outcome == MI_CLS_OUT_PARSE_DROP)
-				odp_atomic_inc_u64(&e->in_errors);
-			if (r.outcome == MI_CLS_OUT_PARSE_DROP) {
-				odp_packet_free(pkt);
-				continue;
-			}
+		if (s->tmp) {
+			rx_enqueue(s->pk, nd, s->tmp, (uint8_t *)(void *)(s->tmp + s->tmp_cap));
 		} else {
-			memset(&r, 0, sizeof(r));
-			r.cos = 0xff;
+			for (int i = 0; i < nd; i++)
+				cos_enq_run(&s->pk[i], 1);
 		}
-		odp_pool_t pool = e->pool;
-
-		if (e->cls_enabled) {
-			if (r.outcome == MI_CLS_OUT_DISCARD || r.outcome == MI_CLS_OUT_LOOP)
-				odp_atomic_inc_u64(&e->in_discards);
-			if (r.outcome != MI_CLS_OUT_ENQ) {
-				odp_packet_free(pkt);
-				continue;
-			}
-			odp_pool_t cp = odp_amd_cls_pool_of(r.cos);
-
-			if (cp != ODP_POOL_INVALID)
-				pool = cp;
-		}
-		/* packet in the final pool (_odp_pktio_packet_to_pool) */
-		if (pkt == ODP_PACKET_INVALID) {
-			pkt = odp_packet_alloc(pool, len);
-			if (pkt == ODP_PACKET_INVALID) {
-				if (e->cls_enabled)
-					odp_atomic_inc_u64(&e->in_discards);
-				continue;
-			}
-			memcpy(odp_packet_data(pkt), s->base + s->soff[i], len);
-		} else if (odp_packet_pool(pkt) != pool) {
-			odp_packet_t np = odp_packet_alloc(pool, len);
-
-			if (np == ODP_PACKET_INVALID) {
-				odp_packet_free(pkt);
-				odp_atomic_inc_u64(&e->in_discards);
-				continue;
-			}
-			pkt_hdr_t *sh = rt_pkt_hdr(pkt);
-
-			memcpy(odp_packet_data(np), sh->head + sh->data_off, len);
-			rt_pkt_hdr(np)->user_ptr = sh->user_ptr;
-			odp_packet_free(pkt);
-			pkt = np;
-		}
-		pkt_hdr_t *h = rt_pkt_hdr(pkt);
-
-		if (layer != ODP_PROTO_LAYER_NONE) {
-			h->in_flags = r.in_flags;
-			h->err = r.err;
-			h->l2 = 0;
-			h->l3 = r.l3_offset;
-			h->l4 = r.l4_offset;
-		} else {
-			h->in_flags = 0;
-			h->err = 0;
-		}
-		h->input = e->hdl;
-		if (!h->err) {
-			octets += len;
-			packets++;
-		}
-		if (e->cls_enabled) {
-			h->cos = r.cos;
-			h->cls_mark = r.mark;
-			h->dst_queue = odp_amd_cls_queue_of(r.cos, r.queue);
-			/* _odp_cls_enq: flush when (dst_queue, cos) changes */
-			if (nrun) {
-				pkt_hdr_t *ph = rt_pkt_hdr(run[nrun - 1]);
-
-				if (ph->dst_queue != h->dst_queue || ph->cos != h->cos) {
-					cos_enq_run(run, nrun);
-					nrun = 0;
-				}
-			}
-			run[nrun++] = pkt;
-		} else if (num_rx < max_out) {
-			out[num_rx++] = pkt;
-		} else {
-			odp_packet_free(pkt);
+	} else {
+		for (int i = 0; i < nd; i++) {
+			if (num_rx < max_out)
+				out[num_rx++] = s->pk[i];
+			else
+				odp_packet_free(s->pk[i]);
 		}
 	}
-	if (nrun)
-		cos_enq_run(run, nrun);
 	e->prof[2] += prof_ns() - t2;
-	odp_atomic_add_u64(&e->in_octets, octets);
-	odp_atomic_add_u64(&e->in_packets, packets);
+	if (c.in_errors)
+		odp_atomic_add_u64(&e->in_errors, c.in_errors);
+	if (c.in_discards)
+		odp_atomic_add_u64(&e->in_discards, c.in_discards);
+	odp_atomic_add_u64(&e->in_octets, c.octets);
+	odp_atomic_add_u64(&e->in_packets, c.packets);
 	return num_rx;
 }
 
