@@ -95,8 +95,8 @@ def build(force: bool = False, out_dir: str = PKG, defines=()) -> list[str]:
               "-o", jitc, jitc_src, "-L", "/opt/rocm/lib", "-lhiprtc", "-Wl,-rpath,/opt/rocm/lib"])
         built.append(jitc)
     if force or _stale(odp_so, odp_srcs + [mi_so] + rt_hdrs):
-        _run(["gcc", "-O2", "-std=gnu11", "-Wall", "-Wextra", "-fPIC", "-shared", "-I", INC,
-              "-o", odp_so] + odp_srcs + ["-L", out_dir, "-lmi_cls", "-Wl,-rpath,$ORIGIN",
+        _run(["gcc", "-O2", "-std=gnu11", "-Wall", "-Wextra", "-fPIC", "-ftls-model=initial-exec",
+              "-shared", "-I", INC, "-o", odp_so] + odp_srcs + ["-L", out_dir, "-lmi_cls", "-Wl,-rpath,$ORIGIN",
                                           "-lpthread"])
         built.append(odp_so)
     if force or _stale(odph_so, [odph_src, odp_so] + rt_hdrs):

@@ -30,6 +30,7 @@
  */
 #define _GNU_SOURCE
 #include <errno.h>
+#include <x86intrin.h>
 #include <inttypes.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -113,7 +114,9 @@ typedef struct {
 	 * previous one is delivered (pipelined receive) */
 	rx_set_t rs[2];
 	int cur;                /* set the next burst is staged into */
-	uint64_t prof[4];       /* ODP_AMD_RX_PROF: ns staging / classifying / delivering, bursts */
+	uint64_t prof[8];       /* ODP_AMD_RX_PROF: ns staging / classifying / delivering, bursts,
+				 * then of delivering: ns preparing / enqueueing, TSC ticks in
+				 * packet allocation / frame copies */
 } rt_pktio_t;
 
 static void rx_sets_free(rt_pktio_t *e);
@@ -783,8 +786,9 @@ int odp_pktio_close(odp_pktio_t h)
 	}
 	if (rx_prof > 0 && e->prof[3])
 		fprintf(stderr, "RXPROF %s bursts %" PRIu64 " stage_ns %" PRIu64 " classify_ns %" PRIu64
-			" deliver_ns %" PRIu64 "\n", e->name, e->prof[3], e->prof[0], e->prof[1],
-			e->prof[2]);
+			" deliver_ns %" PRIu64 " (prepare_ns %" PRIu64 " enqueue_ns %" PRIu64
+			" alloc_tsc %" PRIu64 " copy_tsc %" PRIu64 ")\n", e->name, e->prof[3], e->prof[0],
+			e->prof[1], e->prof[2], e->prof[4], e->prof[5], e->prof[6], e->prof[7]);
 	if (e->inq != ODP_QUEUE_INVALID) {
 		odp_event_t ev[64];
 		int n;
@@ -1211,7 +1215,7 @@ typedef struct {
  * helper threads measured slower -- 14.3 -> 6.4 Mpkt/s with four helpers,
  * profiles/r03g_rx_helpers_ab.txt: each packet's header line then moves between cores
  * on its way to the queue and the consumer -- so one thread does it.) */
-static void rx_prepare(rt_pktio_t *e, rx_set_t *s, int lo, int hi, rx_cnt_t *c)
+static void rx_prepare_each(rt_pktio_t *e, rx_set_t *s, int lo, int hi, rx_cnt_t *c)
 {
 	const odp_proto_layer_t layer = e->parse_layer;
 
@@ -1221,6 +1225,8 @@ static void rx_prepare(rt_pktio_t *e, rx_set_t *s, int lo, int hi, rx_cnt_t *c)
 		uint32_t len = s->slen[i];
 
 		s->pk[i] = ODP_PACKET_INVALID;
+		if (i + 16 < hi)    /* records written by the GPU: not in the CPU caches */
+			__builtin_prefetch(&s->res[i + 16]);
 		if (i + 8 < hi) {   /* frames read in place are cold in the CPU caches */
 			const uint8_t *nf = s->base + s->soff[i + 8];
 			const uint32_t nl = s->slen[i + 8];
@@ -1257,13 +1263,21 @@ static void rx_prepare(rt_pktio_t *e, rx_set_t *s, int lo, int hi, rx_cnt_t *c)
 		}
 		/* packet in the final pool (_odp_pktio_packet_to_pool) */
 		if (pkt == ODP_PACKET_INVALID) {
+			const uint64_t ta = rx_prof > 0 ? __rdtsc() : 0;
+
 			pkt = odp_packet_alloc(pool, len);
 			if (pkt == ODP_PACKET_INVALID) {
 				if (e->cls_enabled)
 					c->in_discards++;
 				continue;
 			}
+			const uint64_t tb = rx_prof > 0 ? __rdtsc() : 0;
+
 			memcpy(odp_packet_data(pkt), s->base + s->soff[i], len);
+			if (rx_prof > 0) {
+				e->prof[6] += tb - ta;
+				e->prof[7] += __rdtsc() - tb;
+			}
 		} else if (odp_packet_pool(pkt) != pool) {
 			odp_packet_t np = odp_packet_alloc(pool, len);
 
@@ -1301,6 +1315,181 @@ static void rx_prepare(rt_pktio_t *e, rx_set_t *s, int lo, int hi, rx_cnt_t *c)
 			h->cls_mark = r.mark;
 			h->dst_queue = odp_amd_cls_queue_of(r.cos, r.queue);
 		}
+		s->pk[i] = pkt;
+	}
+}
+
+
+/* Packet metadata of a delivered frame from its record. */
+static inline void rx_fill(rt_pktio_t *e, pkt_hdr_t *h, const mi_cls_result_t *r, uint32_t len,
+			   rx_cnt_t *c)
+{
+	if (e->parse_layer != ODP_PROTO_LAYER_NONE) {
+		h->in_flags = r->in_flags;
+		h->err = r->err;
+		h->l2 = 0;
+		h->l3 = r->l3_offset;
+		h->l4 = r->l4_offset;
+	} else {
+		h->in_flags = 0;
+		h->err = 0;
+	}
+	h->input = e->hdl;
+	if (!h->err) {
+		c->octets += len;
+		c->packets++;
+	}
+	if (e->cls_enabled) {
+		h->cos = r->cos;
+		h->cls_mark = r->mark;
+		h->dst_queue = odp_amd_cls_queue_of(r->cos, r->queue);
+	}
+}
+
+/* rx_prepare for pcap frames: the same steps in three passes, so packets
+ * are taken from each pool in bulk and their headers prefetched before they
+ * are written (a per-frame odp_packet_alloc spent most of its time on the
+ * cold header line).  Pass 1 decides each frame (parse drop, CoS discard, or
+ * the pool it goes to), pass 2 takes every pool's packets at once -- frames
+ * of one pool get them in arrival order, so when a pool runs short the same
+ * frames are discarded as frame-by-frame allocation would -- and pass 3
+ * initialises the headers, copies the frames and writes the metadata.
+ * `slot` (one byte per frame) and `got` (n_cap packets) are the set's
+ * delivery scratch; more than RX_MAX_POOLS distinct pools in a burst fall
+ * back to rx_prepare_each. */
+#define RX_MAX_POOLS 16
+static void rx_prepare(rt_pktio_t *e, rx_set_t *s, int lo, int hi, rx_cnt_t *c)
+{
+	const odp_proto_layer_t layer = e->parse_layer;
+	uint8_t *slot = s->tmp ? (uint8_t *)(void *)(s->tmp + s->tmp_cap) : NULL;
+	odp_packet_t *got = s->tmp;
+	struct {
+		odp_pool_t pool;
+		uint32_t cap;
+		int cnt, base, have, used;
+	} pl[RX_MAX_POOLS];
+	int npl = 0;
+
+	if (e->drv != DRV_PCAP || !slot) {
+		rx_prepare_each(e, s, lo, hi, c);
+		return;
+	}
+	/* pass 1: the decision per frame */
+	for (int i = lo; i < hi; i++) {
+		if (i + 16 < hi)
+			__builtin_prefetch(&s->res[i + 16]);
+		mi_cls_result_t r;
+		const uint32_t len = s->slen[i];
+
+		s->pk[i] = ODP_PACKET_INVALID;
+		slot[i] = 0xff;
+		if (layer != ODP_PROTO_LAYER_NONE) {
+			r = s->res[i];
+			apply_layer(&r, layer);
+			if (r.err || r.outcome == MI_CLS_OUT_PARSE_DROP)
+				c->in_errors++;
+			if (r.outcome == MI_CLS_OUT_PARSE_DROP)
+				continue;
+		} else {
+			memset(&r, 0, sizeof(r));
+		}
+		odp_pool_t pool = e->pool;
+
+		if (e->cls_enabled) {
+			if (r.outcome == MI_CLS_OUT_DISCARD || r.outcome == MI_CLS_OUT_LOOP)
+				c->in_discards++;
+			if (r.outcome != MI_CLS_OUT_ENQ)
+				continue;
+			odp_pool_t cp = odp_amd_cls_pool_of(r.cos);
+
+			if (cp != ODP_POOL_INVALID)
+				pool = cp;
+		}
+		int k = 0;
+
+		while (k < npl && pl[k].pool != pool)
+			k++;
+		if (k == npl) {
+			rt_pool_t *rp = rt_pool(pool);
+
+			if (npl == RX_MAX_POOLS) {   /* start over frame by frame */
+				memset(c, 0, sizeof(*c));
+				rx_prepare_each(e, s, lo, hi, c);
+				return;
+			}
+			pl[k].pool = pool;
+			pl[k].cap = rp && rp->param.type == ODP_POOL_PACKET ? rp->data_cap : 0u;
+			pl[k].cnt = 0;
+			npl++;
+		}
+		if (len > pl[k].cap) {   /* odp_packet_alloc fails: no packet taken */
+			if (e->cls_enabled)
+				c->in_discards++;
+			continue;
+		}
+		slot[i] = (uint8_t)k;
+		pl[k].cnt++;
+	}
+	/* pass 2: each pool's packets at once */
+	int at = lo;
+
+	for (int k = 0; k < npl; k++) {
+		pl[k].base = at;
+		pl[k].have = pl[k].cnt ? rt_packet_alloc_raw(pl[k].pool, 0, &got[at], pl[k].cnt) : 0;
+		pl[k].used = 0;
+		at += pl[k].cnt;
+	}
+	/* pass 3: headers, frames, metadata */
+	for (int i = lo; i < hi; i++) {
+		if (i + 8 < hi) {   /* frames read in place are cold in the CPU caches */
+			const uint8_t *nf = s->base + s->soff[i + 8];
+			const uint32_t nl = s->slen[i + 8];
+
+			for (uint32_t b = 0; b < nl; b += 64)
+				__builtin_prefetch(nf + b);
+		}
+		const int k = slot[i];
+
+		if (k == 0xff)
+			continue;
+		const int j = pl[k].used++;
+
+		if (j >= pl[k].have) {   /* the pool ran short */
+			if (e->cls_enabled)
+				c->in_discards++;
+			continue;
+		}
+		if (j + 4 < pl[k].have) {   /* a later packet of this pool: its header */
+			const pkt_hdr_t *nh = rt_pkt_hdr(got[pl[k].base + j + 4]);
+
+			/* the buffer follows the 64-B aligned header (odp_rt.c pool
+			 * layout): its first data line, without reading the header */
+			__builtin_prefetch(nh, 1);
+			__builtin_prefetch((const uint8_t *)nh + ((sizeof(pkt_hdr_t) + 63u) & ~(size_t)63u) +
+					   RT_PKT_HEADROOM, 1);
+		}
+		const odp_packet_t pkt = got[pl[k].base + j];
+		const uint32_t len = s->slen[i];
+		mi_cls_result_t r;
+
+		if (layer != ODP_PROTO_LAYER_NONE) {
+			r = s->res[i];
+			apply_layer(&r, layer);
+		} else {
+			memset(&r, 0, sizeof(r));
+			r.cos = 0xff;
+		}
+		const uint64_t ta = rx_prof > 0 ? __rdtsc() : 0;
+
+		rt_packet_init(pkt, len);
+		const uint64_t tb = rx_prof > 0 ? __rdtsc() : 0;
+
+		memcpy(odp_packet_data(pkt), s->base + s->soff[i], len);
+		if (rx_prof > 0) {
+			e->prof[6] += tb - ta;
+			e->prof[7] += __rdtsc() - tb;
+		}
+		rx_fill(e, rt_pkt_hdr(pkt), &r, len, c);
 		s->pk[i] = pkt;
 	}
 }
@@ -1470,8 +1659,18 @@ static int rx_finish(rt_pktio_t *e, rx_set_t *s, odp_packet_t out[], int max_out
 	s->pending = 0;
 	rx_cnt_t c;
 
+	if (!s->tmp || s->tmp_cap < s->n_cap) {
+		/* delivery scratch: packets (bulk allocation, then grouping by
+		 * queue), then one byte per frame (its pool, then its queue group) */
+		free(s->tmp);
+		s->tmp = malloc(s->n_cap * (sizeof(odp_packet_t) + 1u));
+		s->tmp_cap = s->tmp ? s->n_cap : 0;
+	}
 	memset(&c, 0, sizeof(c));
 	rx_prepare(e, s, 0, s->n, &c);
+	const uint64_t t3 = prof_ns();
+
+	e->prof[4] += t3 - t2;
 	/* the delivered packets, compacted in arrival order */
 	int nd = 0, num_rx = 0;
 
@@ -1479,12 +1678,6 @@ static int rx_finish(rt_pktio_t *e, rx_set_t *s, odp_packet_t out[], int max_out
 		if (s->pk[i] != ODP_PACKET_INVALID)
 			s->pk[nd++] = s->pk[i];
 	if (e->cls_enabled) {
-		if (!s->tmp || s->tmp_cap < s->n_cap) {
-			/* grouped packets, then one group index byte per packet */
-			free(s->tmp);
-			s->tmp = malloc(s->n_cap * (sizeof(odp_packet_t) + 1u));
-			s->tmp_cap = s->tmp ? s->n_cap : 0;
-		}
 		if (s->tmp) {
 			rx_enqueue(s->pk, nd, s->tmp, (uint8_t *)(void *)(s->tmp + s->tmp_cap));
 		} else {
@@ -1499,6 +1692,7 @@ static int rx_finish(rt_pktio_t *e, rx_set_t *s, odp_packet_t out[], int max_out
 				odp_packet_free(s->pk[i]);
 		}
 	}
+	e->prof[5] += prof_ns() - t3;
 	e->prof[2] += prof_ns() - t2;
 	if (c.in_errors)
 		odp_atomic_add_u64(&e->in_errors, c.in_errors);

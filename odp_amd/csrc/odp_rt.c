@@ -728,15 +728,25 @@ typedef struct {
 	int n;
 	ev_hdr_t *e[PC_SIZE];
 } pool_cache_t;
-static __thread pool_cache_t *tls_pc[RT_MAX_POOLS];
+/* The thread's caches, one slot per pool, allocated on first use: the TLS
+ * itself is one pointer, so the library builds with the initial-exec TLS
+ * model (a register-relative load instead of a __tls_get_addr call per
+ * packet allocation and free) and still fits the static TLS surplus when it
+ * is dlopen()ed. */
+static __thread pool_cache_t **tls_pc;
 
 static pool_cache_t *pool_cache(rt_pool_t *p)
 {
 	const int idx = (int)(p - RT.pool);
-	pool_cache_t *c = tls_pc[idx];
-
 	if (p->num < PC_MIN_POOL)
 		return NULL;
+	if (!tls_pc) {
+		tls_pc = calloc(RT_MAX_POOLS, sizeof(*tls_pc));
+		if (!tls_pc)
+			return NULL;
+	}
+	pool_cache_t *c = tls_pc[idx];
+
 	if (!c) {
 		c = calloc(1, sizeof(*c));
 		if (!c)
@@ -753,7 +763,7 @@ static pool_cache_t *pool_cache(rt_pool_t *p)
 
 static void pool_cache_flush(int idx)
 {
-	pool_cache_t *c = tls_pc[idx];
+	pool_cache_t *c = tls_pc ? tls_pc[idx] : NULL;
 
 	if (c && c->n && RT.pool[idx].used && c->gen == RT.pool[idx].gen)
 		pool_give(&RT.pool[idx], c->e, c->n);
@@ -767,7 +777,7 @@ uint32_t rt_pool_avail(odp_pool_t h)
 
 	if (!p)
 		return 0;
-	const pool_cache_t *c = tls_pc[p - RT.pool];
+	const pool_cache_t *c = tls_pc ? tls_pc[p - RT.pool] : NULL;
 
 	return p->num_free + (c && c->gen == p->gen ? (uint32_t)c->n : 0u);
 }
@@ -854,6 +864,20 @@ int odp_packet_alloc_multi(odp_pool_t pool, uint32_t len, odp_packet_t pkt[], in
 			break;
 	}
 	return done;
+}
+
+int rt_packet_alloc_raw(odp_pool_t pool, uint32_t len, odp_packet_t pkt[], int num)
+{
+	rt_pool_t *p = rt_pool(pool);
+
+	if (!p || p->param.type != ODP_POOL_PACKET || len > p->data_cap || num <= 0)
+		return 0;
+	return pool_alloc(p, (ev_hdr_t **)(void *)pkt, num);
+}
+
+void rt_packet_init(odp_packet_t pkt, uint32_t len)
+{
+	pkt_init(rt_pkt_hdr(pkt), len);
 }
 
 odp_packet_t odp_packet_alloc(odp_pool_t pool, uint32_t len)

@@ -102,6 +102,11 @@ rt_pool_t *rt_pool(odp_pool_t pool);
 /* free events of a pool this thread can allocate: its free list plus the
  * calling thread's cache */
 uint32_t rt_pool_avail(odp_pool_t pool);
+/* up to num packets of a pool whose buffers hold len bytes, headers NOT
+ * initialised (rt_packet_init does that, e.g. after a prefetch); returns the
+ * count taken */
+int rt_packet_alloc_raw(odp_pool_t pool, uint32_t len, odp_packet_t pkt[], int num);
+void rt_packet_init(odp_packet_t pkt, uint32_t len);
 int rt_queue_enq_multi(rt_queue_t *q, const odp_event_t ev[], int num);
 int rt_queue_deq_multi_raw(rt_queue_t *q, odp_event_t ev[], int num);
 int rt_thread_id(void);

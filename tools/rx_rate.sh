@@ -5,6 +5,7 @@
 set -o pipefail
 OUT=${1:-gpurun_out/rx}
 mkdir -p $OUT
+trap 'rm -f $OUT/in.pcap' EXIT
 timeout -k 10 120 python - "$OUT" ${2:-200000} <<'PY' || exit 1
 import sys
 sys.path.insert(0, ".")
@@ -25,4 +26,3 @@ run sched sched NONE=1
 run direct_sync direct ODP_AMD_RX_PIPELINE=0
 run direct_staged direct ODP_AMD_RX_INPLACE=0
 run direct_sync_staged direct ODP_AMD_RX_PIPELINE=0 ODP_AMD_RX_INPLACE=0
-rm -f $OUT/in.pcap
