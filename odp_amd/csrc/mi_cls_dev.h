@@ -645,26 +645,30 @@ __device__ __forceinline__ uint32_t wave_scan_xor(uint32_t v, uint32_t lane)
 }
 
 // Wave-cooperative CRC-32C of the SCTP check (all 64 lanes active): lane f
-// asks for the CRC over frame bytes [l4, len) of its frame (batch offset
-// boff) with the checksum field [l4 + 8, l4 + 12) taken as zero, init ~0,
-// inverted -- `cnt` = ceil((len - l4) / 64) pieces of 64 B counted from the
-// END of the frame (piece m = [len - 64 (m+1), len - 64 m)), dealt out 64 per
-// round as in ck_sum_wave.  CRC is linear over GF(2): a lane computes the
-// raw CRC (init 0) of its piece, bytes below l4 and the checksum field as
-// zero -- leading zeros leave a zero register unchanged, and pieces aligned
-// to the end have no trailing partial block -- and shifts it by the 64 m
-// bytes after it (x^(512 m), table z); the frame's register is the XOR of
-// its pieces' (prefix XOR over the round), plus the init's contribution
-// ~0 * x^(8 (len - l4)).  Returns the finished CRC for the asking lanes.
+// asks (ask != 0) for the CRC over frame bytes [l4, len) of its frame (batch
+// offset boff) with the checksum field [l4 + 8, l4 + 12) taken as zero, init
+// ~0, inverted.  The bytes are cut into the nf = (len - l4) / 64 full 64-B
+// pieces counted from l4 and a last partial piece of r = (len - l4) % 64
+// bytes.  The full pieces of all lanes are dealt out 64 per round as in
+// ck_sum_wave (16-B loads from l4 on: no byte below l4 is ever read into a
+// CRC, and the checksum field is dword 2 of piece 0, so no masks).  CRC is
+// linear over GF(2): a lane computes the raw CRC (init 0) of its piece and
+// shifts it by the full pieces after it, x^(512 (nf - 1 - k)) (table z); the
+// frame's register is the XOR of its pieces' (prefix XOR over the round),
+// shifted once more by the r partial bytes (x^(8 r), table y), XOR the raw
+// CRC of the partial piece (its owner lane walks it: <= 15 words + 3 bytes),
+// plus the init's contribution ~0 * x^(8 (len - l4)).  Returns the finished
+// CRC for the asking lanes.
 __device__ __forceinline__ uint32_t sctp_crc_wave(__amdgpu_buffer_rsrc_t rs, uint32_t boff,
-						  uint32_t l4, uint32_t len, uint32_t cnt,
+						  uint32_t l4, uint32_t len, uint32_t ask,
 						  uint32_t lane, const uint32_t *tab)
 {
 	const uint32_t *zt = tab + 1024u, *yt = zt + CRC_ZN;
-	const uint32_t incl = wave_scan_add(cnt, lane);
-	const uint32_t first = incl - cnt;
+	const uint32_t n = ask ? len - l4 : 0u, nf = n >> 6, rr = n & 63u;
+	const uint32_t incl = wave_scan_add(nf, lane);
+	const uint32_t first = incl - nf;
 	const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, WAVE - 1);
-	const uint32_t geo = l4 | (len << 16);
+	const uint32_t p0 = boff + l4;   // batch offset of the first L4 byte
 	uint32_t acc = 0;
 	for (uint32_t B = 0; B < total; B += WAVE) {
 		const uint32_t g = B + lane;
@@ -674,38 +678,22 @@ __device__ __forceinline__ uint32_t sctp_crc_wave(__amdgpu_buffer_rsrc_t rs, uin
 			const uint32_t c = lo + st;
 			lo = lane_get(first, c) <= g ? c : lo;
 		}
-		const uint32_t m = g - lane_get(first, lo);   // piece number from the end
-		const uint32_t gg = lane_get(geo, lo);
-		const uint32_t ob = lane_get(boff, lo);
+		const uint32_t k = g - lane_get(first, lo);   // piece number from l4
+		const uint32_t fnf = lane_get(nf, lo);
+		const uint32_t ob = lane_get(p0, lo) + 64u * k;
 		const bool live = g < total;
-		const int32_t fl4 = (int32_t)(gg & 0xffffu), flen = (int32_t)(gg >> 16);
-		const int32_t start = flen - 64 * (int32_t)(m + 1u);   // frame-relative
 		u32x4 v[4];
 #pragma unroll
-		for (int32_t i = 0; i < 4; ++i) {
-			// 16-B pieces wholly below l4 are not needed; pieces starting
-			// before the batch read as zero (OOB offset), bytes below l4
-			// are masked anyway
-			const int32_t o = start + 16 * i;
-			const bool need = live && o + 16 > fl4;
-			v[i] = __builtin_amdgcn_raw_buffer_load_b128(
-				rs, (need && (int32_t)ob + o >= 0) ? (uint32_t)((int32_t)ob + o) : OOB_OFF, 0, 0);
-		}
+		for (uint32_t i = 0; i < 4; ++i)
+			v[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, live ? ob + 16u * i : OOB_OFF, 0, 0);
 		uint32_t crc = 0;
-		const int32_t rel = fl4 - start;   // l4 relative to the piece start
 #pragma unroll
-		for (int32_t d = 0; d < 16; ++d) {
-			const int32_t a = rel - 4 * d;         // l4 relative to this dword
-			// keep bytes >= l4, drop the checksum field [l4 + 8, l4 + 12)
-			const uint32_t lo_cut = (uint32_t)min(max(a, 0), 4);
-			const uint32_t f0 = (uint32_t)min(max(a + 8, 0), 4), f1 = (uint32_t)min(max(a + 12, 0), 4);
-			const uint64_t ones = 0xFFFFFFFFull;
-			const uint32_t keep = (uint32_t)(ones << (8u * lo_cut)) &
-					      ~((uint32_t)(ones << (8u * f0)) & ~(uint32_t)(ones << (8u * f1)));
-			crc = crc32c_u32(tab, crc, v[d >> 2][d & 3] & keep);
+		for (uint32_t d = 0; d < 16; ++d) {
+			const uint32_t w = v[d >> 2][d & 3];
+			crc = crc32c_u32(tab, crc, (d == 2u && k == 0u) ? 0u : w);   // the checksum field
 		}
-		// shift by the 64 m bytes after the piece
-		const uint32_t r = live ? crc_mulmod(crc, zt[min(m, (uint32_t)CRC_ZN - 1u)]) : 0u;
+		// shift by the full pieces after this one
+		const uint32_t r = live ? crc_mulmod(crc, zt[min(fnf - 1u - k, (uint32_t)CRC_ZN - 1u)]) : 0u;
 		const uint32_t P = wave_scan_xor(r, lane);
 		const uint32_t a0 = first > B ? first - B : 0u;
 		const uint32_t e = min(incl > B ? incl - B : 0u, (uint32_t)WAVE);
@@ -713,8 +701,42 @@ __device__ __forceinline__ uint32_t sctp_crc_wave(__amdgpu_buffer_rsrc_t rs, uin
 		const uint32_t pa = lane_get(P, a0 > 0u ? a0 - 1u : 0u);
 		acc ^= (e > a0) ? (pe ^ (a0 > 0u ? pa : 0u)) : 0u;
 	}
+	// the full pieces sit rr bytes before the frame end
+	acc = (ask && nf) ? crc_mulmod(acc, yt[rr]) : 0u;
+	// the partial piece, walked by its owner: words, then 0-3 bytes
+	{
+		const uint32_t pb = p0 + 64u * nf;   // its first byte
+		u32x4 v[4];
+#pragma unroll
+		for (uint32_t i = 0; i < 4; ++i)
+			v[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (ask && 16u * i < rr) ? pb + 16u * i
+									     : OOB_OFF, 0, 0);
+		uint32_t crc = 0;
+#pragma unroll
+		for (uint32_t d = 0; d < 15; ++d) {
+			const uint32_t w = v[d >> 2][d & 3];
+			if (__ballot(ask && 4u * d + 4u <= rr) != 0ull) {
+				if (ask && 4u * d + 4u <= rr)
+					crc = crc32c_u32(tab, crc, (d == 2u && nf == 0u) ? 0u : w);
+			}
+		}
+		// the word holding the tail bytes (selects: no dynamic register index)
+		const uint32_t q = rr >> 2;
+		uint32_t wl = 0u;
+#pragma unroll
+		for (uint32_t d = 0; d < 16; ++d)
+			wl = d == q ? v[d >> 2][d & 3] : wl;
+#pragma unroll
+		for (uint32_t b = 0; b < 3; ++b) {
+			// a tail byte of the checksum field (frames of < 12 L4 bytes) is zero
+			const uint32_t o = 4u * q + b;
+			const bool in = ask && o < rr;
+			const uint32_t byte = (nf == 0u && o >= 8u && o < 12u) ? 0u : ((wl >> (8u * b)) & 0xffu);
+			crc = in ? crc32c_u8(tab, crc, byte) : crc;
+		}
+		acc ^= crc;
+	}
 	// the init register ~0 shifted over the whole message
-	const uint32_t n = len - l4;
 	const uint32_t sh = crc_mulmod(zt[min(n >> 6, (uint32_t)CRC_ZN - 1u)], yt[n & 63u]);
 	return ~(acc ^ crc_mulmod(0xFFFFFFFFu, sh));
 }
@@ -766,8 +788,7 @@ __device__ __forceinline__ void l4_chksum(const Pkt &k, Parsed &p, uint32_t opt,
 		// frames with at most CRC_ZN 64-B pieces: the wave cooperates;
 		// longer (jumbo) ones: one lane walks its frame
 		const bool wv = kind == 3u && len - l4 < 64u * CRC_ZN;
-		const uint32_t crc = sctp_crc_wave(rs, boff, l4, len, wv ? (len - l4 + 63u) >> 6 : 0u,
-						   lane, crc_tab);
+		const uint32_t crc = sctp_crc_wave(rs, boff, l4, len, wv ? 1u : 0u, lane, crc_tab);
 		if (wv)
 			bad = crc != r32(k, l4 + 8u);
 		if (__ballot(kind == 3u && !wv) != 0ull) {

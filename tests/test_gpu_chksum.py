@@ -145,3 +145,31 @@ def test_sctp_crc_long_frames(built, gpu):
     got = both([R.cos("d", queue=1), ("default", 0)], b, CK.SCTP_CK, "sctp long")
     assert ((got["in_flags"] >> 31) & 1).all()
     assert np.array_equal((got["err"] & CK.E_L4CK) != 0, bad)
+
+
+@pytest.mark.parametrize("ipver", [4, 6])
+def test_sctp_crc_every_piece_split(built, gpu, ipver):
+    """SCTP CRC-32C at every L4 length from 12 to 395 bytes: no full 64-B
+    piece (the checksum field in the owner's partial piece), one to six full
+    pieces with partial pieces of every size 0..63; valid, and with the
+    checksum's last byte flipped in every 3rd frame: GPU == oracle, verdicts
+    as constructed."""
+    rng = np.random.default_rng(90 + ipver)
+    l4 = 14 + (20 if ipver == 4 else 40)
+    lens = np.arange(l4 + 12, l4 + 396)
+    n = lens.size
+    kw = dict(sip4=rng.integers(0, 2**32, n).astype(np.uint64),
+              dip4=rng.integers(0, 2**32, n).astype(np.uint64)) if ipver == 4 else dict(
+        sip6=rng.integers(0, 256, (n, 16), dtype=np.uint8),
+        dip6=rng.integers(0, 256, (n, 16), dtype=np.uint8))
+    b = pg.build_batch(lens, ipver=np.full(n, ipver), l4proto=np.full(n, pg.IPPROTO_SCTP),
+                       sport=rng.integers(1, 65535, n), dport=rng.integers(1, 65535, n), seed=9,
+                       **kw)
+    pg.set_checksums(b)
+    bad = np.zeros(n, bool)
+    for i in range(0, n, 3):
+        b.buf[int(b.off[i]) + l4 + 11] ^= 0x01   # the CRC field's last byte
+        bad[i] = True
+    got = both([R.cos("d", queue=1), ("default", 0)], b, CK.SCTP_CK, f"sctp splits ipv{ipver}")
+    assert ((got["in_flags"] >> 31) & 1).all()
+    assert np.array_equal((got["err"] & CK.E_L4CK) != 0, bad)
