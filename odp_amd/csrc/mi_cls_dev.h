@@ -1338,6 +1338,11 @@ struct DescU {
 	// 16 words at hot-region word o (a direct block's shared class record)
 	__device__ __forceinline__ DescV root(uint32_t o) const { return DescU{ h + o, h }.vec(0u); }
 };
+// Engine value of a program-specialised kernel whose default CoS has a chain
+// of blocks (flat programs only): the blocks, their offsets and engines are
+// the spec's constants (S::nblk, S::boff, S::bmode).
+#define FM_CHAIN 5
+
 // A classification block known when the kernel is compiled (program-
 // specialised kernels, mi_cls_spec.cpp): S::blk holds the default CoS's block
 // words (header and class records, zero-padded by 16 words) and S::root a
@@ -1727,6 +1732,28 @@ __device__ __forceinline__ uint32_t bv_first(const D &blk, const DescV &hb, T H,
 	return first;
 }
 
+template <typename D> struct SpecOf {
+	typedef void type;
+};
+template <typename S> struct SpecOf<DescC<S>> {
+	typedef S type;
+};
+
+// First holding rule over a compile-time chain (FM_CHAIN): block I and on,
+// each with its engine compiled in; the smallest over the chain.
+template <typename S, uint32_t I = 0, typename T>
+__device__ __forceinline__ uint32_t chain_first(T H, cword_t hc, bool act, const Pkt &k,
+						const Parsed &p, const Fields &x)
+{
+	if constexpr (I >= S::nblk) {
+		return BV_NONE;
+	} else {
+		const DescC<S> b{ S::boff[I], hc };
+		const uint32_t f = bv_first<(int)S::bmode[I], false>(b, b.hdr(), H, act, k, p, x);
+		return min(f, chain_first<S, I + 1>(H, hc, act, k, p, x));
+	}
+}
+
 // Classification block evaluation of one CoS for the lanes in `act`
 // (see build_bv for the two modes).  `blk` reads the CoS's block (wave-
 // uniform or per lane); H is the hot region the block's offsets index.  On
@@ -1769,7 +1796,10 @@ __device__ __forceinline__ void bv_eval(const D &blk, T H, bool act, const Pkt &
 		return;
 	}
 	uint32_t first;
-	if constexpr (CHAIN && FM < 0 && std::is_same<D, DescU>::value) {
+	if constexpr (FM == FM_CHAIN) {
+		// a chain compiled into a specialised kernel
+		first = chain_first<typename SpecOf<D>::type>(H, blk.h, act, k, p, x);
+	} else if constexpr (CHAIN && FM < 0 && std::is_same<D, DescU>::value) {
 		// a chain (wave-uniform blocks only): one copy of the engines,
 		// looping over the blocks
 		first = BV_NONE;

@@ -212,14 +212,16 @@ def test_classify_without_gpu_fails_loudly(c):
     assert rc < 0        # -ENODEV: no CPU fallback exists
 
 
-@pytest.mark.parametrize("cfg,flat", [(2, True), (3, True), (4, True), ("nested1024", True),
-                                      (5, False), ("classes", False), ("noblock", False)])
-def test_specialised_kernel_compiles(built, cfg, flat):
+@pytest.mark.parametrize("cfg,flat,spec", [(2, True, True), (3, True, True), (4, True, True),
+                                           ("nested1024", True, True), (5, False, False),
+                                           ("classes", False, True), ("noblock", False, False)])
+def test_specialised_kernel_compiles(built, cfg, flat, spec):
     """The embedded kernel sources compile with hipRTC (no GPU needed) into
     the program-specialised kernel of a flat program (every packet decided
-    on the default CoS's block in one round; candidate lists included); CoS
-    trees (config 5), chains of blocks (9 key classes) and a default CoS
-    without rules have none."""
+    on the default CoS's block in one round; candidate lists included) and
+    of a flat program whose default CoS has a chain of blocks (9 key
+    classes: no generic flat kernel, the chain compiled in); CoS trees
+    (config 5) and a default CoS without rules have none."""
     L = cls.lib()
     L.mi_cls_spec_compile.restype = C.c_int
     L.mi_cls_spec_compile.argtypes = [C.c_void_p, C.c_size_t, C.c_int]
@@ -238,7 +240,7 @@ def test_specialised_kernel_compiles(built, cfg, flat):
         blob = c.compile()
         assert (c.program_info()["flat_engine"] >= 0) == flat
         for nw in ((4, 16) if cfg == 3 else (16,)):
-            assert L.mi_cls_spec_compile(blob, len(blob), nw) == (0 if flat else 1)
+            assert L.mi_cls_spec_compile(blob, len(blob), nw) == (0 if spec else 1)
     finally:
         c.close()
 
