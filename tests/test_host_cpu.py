@@ -268,3 +268,18 @@ def test_block_chain_for_many_classes(built):
             assert i3["tree"] and i3["chained"] == 0, i3
     finally:
         c.close()
+
+
+def test_shadowed_rules_leave_candidate_lists(built):
+    """A rule that can hold only when an earlier rule holds is dropped at
+    block build (it is never the first holding rule): the nested-prefix ACL
+    with 1024 rules, whose /20 lines repeat, then gets the single-candidate
+    engine instead of candidate lists (parity: tests/test_gpu_parity.py
+    test_overlapping_acls, every engine forcing)."""
+    c = cls.Classifier(gpu=0)
+    try:
+        c.apply(R.config3_nested(100, scale=4)[1])
+        info = c.program_info()
+        assert info["cand1"] == 1 and info["candidate"] == 0, info
+    finally:
+        c.close()
