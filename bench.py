@@ -71,6 +71,12 @@ def parse_args():
     ap.add_argument("--no-extra", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--no-runtime", action="store_true",
+                    help="skip the ODP runtime receive-rate leg of e2e")
+    ap.add_argument("--extras-json", default=None,
+                    help="(internal) run only the extra configurations and write them to this "
+                         "file: the main process runs them in a child process, so a failure "
+                         "there cannot cost the headline line")
     ap.add_argument("--timed-only", action="store_true",
                     help="only the timed single-config pass (profiling runs)")
     ap.add_argument("--pktin-opt", type=lambda x: int(x, 0), default=0,
@@ -382,20 +388,24 @@ def bench_cfg(cls, cfg, a, dev, local, steps, warmup, pktin_opt=0, parity=True, 
         c2.set_pktin_opt(pktin_opt)
     log("  rules loaded, waiting for the specialised kernel")
     spec = c2.spec_wait() == 0 and not pktin_opt
-    log(f"  specialised={spec}, timing")
     info = c2.program_info()
     engine = ("linear scan" if info["blocks"] == 0 else
               ["direct", "candidate lists", "bitmap", "wide bitmap", "single candidate"][
                   [info["direct"], info["candidate"], info["bitmap"], info["wide"],
                    info["cand1"]].index(max(info["direct"], info["candidate"], info["bitmap"],
                                             info["wide"], info["cand1"]))])
+    # the instantiation the launches take, logged before the first timed
+    # launch (a fault record then names it)
+    launch = predicted_launch(c2, b2, dev)
+    log(f"  specialised={spec}, engine={engine}, kernel {launch['name']}: timing")
     w1, k1, t_out = time_device(c2, b2, dev, steps, warmup, rotate=a.rotate)
+    launch = c2.last_launch()
     got = records(t_out, b2.n).copy()
     w2, _, _ = time_device(c2, b2, dev, steps, warmup, rotate=a.rotate, streams=2)
     c2.close()
     nbytes = (int(b2.len.astype(np.int64).sum()) + 22 * b2.n) if full_bytes else b2.header_bytes()
     e = {"workload": WORKLOAD[cfg], "rules": R.rule_count(p2), "engine": engine,
-         "specialised": spec,
+         "specialised": spec, "launch": launch,
          "mpkts_per_s": round(b2.n * steps / w1 / 1e6, 2),
          "mpkts_per_s_2streams": round(b2.n * steps / w2 / 1e6, 2),
          "kernel_ms": round(k1, 5), "bytes_per_launch": nbytes,
@@ -417,6 +427,68 @@ def bench_cfg(cls, cfg, a, dev, local, steps, warmup, pktin_opt=0, parity=True, 
         else:
             e["parity_vs_oracle"] = oracle_parity(o_prog, b2, got)
     return e
+
+
+def predicted_launch(c, batch, dev):
+    """One launch over the batch's first 64 packets (same rules, same
+    options: the kernel choice does not depend on n), returning the
+    instantiation the timed launches will take."""
+    import torch
+    small = batch.slice(0, min(64, batch.n))
+    tb, to, tl, tout = to_device(small, dev)
+    rc = c.classify_device(tb.data_ptr(), to.data_ptr(), tl.data_ptr(), small.n, tout.data_ptr(),
+                           torch.cuda.current_stream(dev).cuda_stream)
+    if rc:
+        raise RuntimeError(f"classify failed: {rc}")
+    torch.cuda.synchronize(dev)
+    return c.last_launch()
+
+
+def run_extras(a, dev, local):
+    """The extra configurations (this process: --extras-json)."""
+    from odp_amd import cls
+    extra = {}
+    k_steps = max(5, a.steps // 2)
+    for cfg in (33, 2, 4, 5, 36, 37, 38):
+        if cfg == a.config:
+            continue
+        extra[WORKLOAD[cfg]] = bench_cfg(cls, cfg, a, dev, local, k_steps, 3,
+                                         parity=not a.no_parity)
+    # pktin checksum validation (IPv4 header, UDP/TCP sums over the whole
+    # frame): config 3 IMIX with valid checksums; the kernel reads every
+    # frame byte, so the bytes are frame + 22 B
+    extra["config3_checksums"] = bench_cfg(cls, 3, a, dev, local, k_steps, 3, pktin_opt=0x3C,
+                                           parity=not a.no_parity, full_bytes=True)
+    # the same with a third of the packets SCTP (CRC-32C over the whole frame)
+    extra["config3_sctp_checksums"] = bench_cfg(cls, 35, a, dev, local, k_steps, 3,
+                                                pktin_opt=0x3C, parity=not a.no_parity,
+                                                full_bytes=True)
+    return extra
+
+
+def extras_child(a):
+    """Run the extras in a child process (started, not exec'd: this process
+    has initialised the GPU) and return their entries, or an error entry
+    with the child's exit status -- the headline line is printed either way."""
+    import subprocess
+    import tempfile
+    fd, path = tempfile.mkstemp(prefix="bench_extra_", suffix=".json")
+    os.close(fd)
+    cmd = [sys.executable, os.path.abspath(__file__), "--extras-json", path,
+           "--steps", str(a.steps), "--warmup", str(a.warmup), "--config", str(a.config),
+           "--packets", str(a.n), "--rotate", str(a.rotate)]
+    if a.no_parity:
+        cmd.append("--no-parity")
+    try:
+        rc = subprocess.call(cmd, timeout=900)   # progress lines go straight to stderr
+        if rc != 0:
+            return {"error": f"extras process exited with status {rc}"}
+        with open(path) as f:
+            return json.load(f)
+    except subprocess.TimeoutExpired:
+        return {"error": "extras process timed out (900 s)"}
+    finally:
+        os.unlink(path)
 
 
 def launch_ranks(n):
@@ -469,6 +541,11 @@ def main():
     dev = torch.device(f"cuda:{local}")
 
     from odp_amd import cls, rules as R
+    if a.extras_json:
+        extra = run_extras(a, dev, local)
+        with open(a.extras_json, "w") as f:
+            json.dump(extra, f)
+        return
     # The node's capture is world x n packets; rank r classifies slice r of
     # it, cut by the product's multi-GPU sharding (mi_cls_shard, the cut
     # mi_cls_group_classify_host makes: contiguous, balanced by header
@@ -498,10 +575,12 @@ def main():
     # rule load is control plane: the program-specialised kernel (compiled in
     # the background after the rules are loaded) is ready before timing
     spec = c.spec_wait() == 0
-    log(f"specialised={spec}, timing")
+    launch = predicted_launch(c, batch, dev)
+    log(f"specialised={spec}, kernel {launch['name']}: timing")
 
     wall, kms, t_out = time_device(c, batch, dev, a.steps, a.warmup, dist_on, a.rotate,
                                    a.streams)
+    launch = c.last_launch()
     red_dev = dev if backend == "nccl" else torch.device("cpu")   # where reductions run
     if dist_on:
         t = torch.tensor([wall], dtype=torch.float64, device=red_dev)
@@ -547,6 +626,7 @@ def main():
                          "traffic": (pmc or {}).get("hbm_bytes_per_launch"),
                          "kernel": "mi_cls_kernel" + (" (program-specialised)" if spec and
                                                        not a.pktin_opt else ""),
+                         "launch": launch,
                          "kernel_ms": round(kms, 5),
                          "bytes_per_launch": bytes_launch,
                          "traffic_source": (pmc or {}).get("source")},
@@ -566,34 +646,18 @@ def main():
                 line["e2e"] = time_e2e(c, batch, dev)
             except Exception as e:   # recorded, never fatal
                 line["e2e"] = {"error": str(e)}
-            log("ODP runtime receive rate")
-            try:
-                line["e2e"]["runtime"] = time_runtime(batch, prog)
-            except Exception as e:   # recorded, never fatal
-                line["e2e"]["runtime"] = {"error": str(e)}
+            if not a.no_runtime:
+                log("ODP runtime receive rate")
+                try:
+                    line["e2e"]["runtime"] = time_runtime(batch, prog)
+                except Exception as e:   # recorded, never fatal
+                    line["e2e"]["runtime"] = {"error": str(e)}
             if not a.no_cpu:
                 log("cpu baseline")
                 line["cpu_baseline"] = cpu_baseline(prog, batch, a.cpu_seconds)
             if not a.no_extra:
-                extra = {}
-                k_steps = max(5, a.steps // 2)
-                for cfg in (33, 2, 4, 5, 36, 37, 38):
-                    if cfg == a.config:
-                        continue
-                    extra[WORKLOAD[cfg]] = bench_cfg(cls, cfg, a, dev, local, k_steps, 3,
-                                                     parity=not a.no_parity)
-                # pktin checksum validation (IPv4 header, UDP/TCP sums over the
-                # whole frame): config 3 IMIX with valid checksums; the kernel
-                # reads every frame byte, so the bytes are frame + 22 B
-                extra["config3_checksums"] = bench_cfg(cls, 3, a, dev, local, k_steps, 3,
-                                                       pktin_opt=0x3C, parity=not a.no_parity,
-                                                       full_bytes=True)
-                # the same with a third of the packets SCTP (CRC-32C over the
-                # whole frame, slicing-by-4 per lane)
-                extra["config3_sctp_checksums"] = bench_cfg(cls, 35, a, dev, local, k_steps, 3,
-                                                            pktin_opt=0x3C, parity=not a.no_parity,
-                                                            full_bytes=True)
-                line["extra"] = extra
+                log("extras (child process)")
+                line["extra"] = extras_child(a)
         res = line
         print(json.dumps(res), flush=True)
     c.close()

@@ -235,6 +235,23 @@ int mi_cls_spec_wait(mi_cls_ctx_t *ctx);
  * kernel sources build. */
 int mi_cls_spec_compile(const void *tbl, size_t bytes, int nw);
 
+/* State of the specialised-kernel compiler (host only): *running = compiler
+ * processes alive (at most 1: one compile at a time), *queued = 1 if a
+ * request waits to start (a newer request replaces it), *cached = distinct
+ * programs kept (at most 64; later programs run the generic kernels).
+ * Returns 1 while the compile thread is active, else 0. */
+int mi_cls_spec_pending(uint32_t *running, uint32_t *queued, uint32_t *cached);
+
+/* The kernel instantiation the context's last mi_cls_classify launched
+ * (diagnostics: bench lines and fault records name it).  info[0] waves per
+ * block, [1] 1 if the hot region was in LDS, [2] 1 if the per-lane CoS-tree
+ * rounds were compiled in (DIV), [3] flat engine + 1 (0: not a flat
+ * kernel), [4] 1 if program-specialised, [5] 1 if the pktin-option kernel
+ * (CK), [6] grid (blocks).  All zero before the first launch.  Returns the
+ * number of words written (min(n, MI_CLS_LAUNCH_INFO_WORDS)) or -EINVAL. */
+#define MI_CLS_LAUNCH_INFO_WORDS 7
+int mi_cls_last_launch(const mi_cls_ctx_t *ctx, uint32_t *info, uint32_t n);
+
 /* ------------------------------------------------------------------------
  * Multi-GPU: one host batch over several devices.
  * The batch shards with no exchange step: mi_cls_shard cuts it into

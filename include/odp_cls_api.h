@@ -306,6 +306,11 @@ int odp_amd_cls_classify_host_wait(odp_pktio_t pktio, uint64_t ticket);
  * < 0 error. */
 int odp_amd_cls_spec_wait(odp_pktio_t pktio);
 
+/* The kernel instantiation of the pktio's last device launch
+ * (mi_cls_last_launch: waves per block, LDS hot region, DIV, flat engine + 1,
+ * specialised, pktin-option kernel, grid). */
+int odp_amd_cls_last_launch(odp_pktio_t pktio, uint32_t *info, uint32_t n);
+
 /* Create the device context, upload the current rule snapshot and run a
  * warm-up launch (odp_pktio_start). */
 int odp_amd_cls_prepare(odp_pktio_t pktio, int parse_only);

@@ -125,7 +125,8 @@ def write_src_inc(path, defines=()):
     defs = ", ".join(f'"-D{d}"' for d in defines)
     with open(path, "w") as f:
         f.write(lit("mi_cls_src_h", h) + lit("mi_cls_src_dev", dev) +
-                f"static const char *const mi_cls_src_defs[] = {{ {defs}{', ' if defs else ''}nullptr }};\n")
+                f"static const char *const mi_cls_src_defs[] = {{ {defs}{', ' if defs else ''}nullptr }};\n"
+                f'static const char mi_cls_src_arch[] = "{ARCH}";\n')
 
 
 TEST_BIN = os.path.join(ROOT, "tests", "_bin")

@@ -143,6 +143,9 @@ def _load():
         "odp_amd_cls_pktin_opt_set": (i32, [vp, C.c_uint64]),
         "odp_amd_cls_spec_wait": (i32, [vp]),
         "mi_cls_spec_wait": (i32, [vp]),
+        "odp_amd_cls_last_launch": (i32, [vp, C.POINTER(u32), u32]),
+        "mi_cls_last_launch": (i32, [vp, C.POINTER(u32), u32]),
+        "mi_cls_spec_pending": (i32, [C.POINTER(u32), C.POINTER(u32), C.POINTER(u32)]),
         "mi_cls_device_count": (i32, []),
         "mi_cls_ctx_create": (i32, [i32, C.POINTER(vp)]),
         "mi_cls_ctx_destroy": (i32, [vp]),
@@ -191,6 +194,13 @@ class PinnedArray:
         if self.ptr:
             lib().mi_cls_host_free(self.ptr)
             self.ptr = None
+
+
+def spec_pending() -> dict:
+    """Specialised-kernel compiler state (mi_cls_spec_pending)."""
+    r, q, c = C.c_uint32(), C.c_uint32(), C.c_uint32()
+    active = lib().mi_cls_spec_pending(C.byref(r), C.byref(q), C.byref(c))
+    return {"active": bool(active), "running": r.value, "queued": q.value, "cached": c.value}
 
 
 def lib():
@@ -329,6 +339,21 @@ class Classifier:
         if rc < 0:
             raise RuntimeError(f"odp_amd_cls_spec_wait: {rc}")
         return rc
+
+    def last_launch(self) -> dict:
+        """The kernel instantiation of the last device launch
+        (odp_amd_cls_last_launch)."""
+        info = (C.c_uint32 * 7)()
+        rc = self.L.odp_amd_cls_last_launch(self.pktio, info, 7)
+        if rc < 0:
+            raise RuntimeError(f"odp_amd_cls_last_launch: {rc}")
+        k = {"nw": info[0], "lds_hot": bool(info[1]), "div": bool(info[2]),
+             "flat_engine": int(info[3]) - 1, "specialised": bool(info[4]), "ck": bool(info[5]),
+             "grid": info[6]}
+        k["name"] = (f"mi_cls_kernel<LT={int(k['lds_hot'])}, DIV={int(k['div'])}, NW={k['nw']}, "
+                     f"FM={k['flat_engine']}, CK={int(k['ck'])}"
+                     f"{', MiSpec' if k['specialised'] else ''}>")
+        return k
 
     # -- data path -------------------------------------------------------
     def classify_device(self, d_buf, d_off, d_len, n, d_out, stream=0):

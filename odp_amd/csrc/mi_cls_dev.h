@@ -2501,12 +2501,40 @@ int mi_cls_launch_flat(int nw, int fm, unsigned grid, size_t dyn, hipStream_t st
 int mi_cls_launch_ck(int nw, bool lt, bool div, unsigned grid, size_t dyn, hipStream_t st,
 		     const KArgs &a);
 
-#endif   // !__HIPCC_RTC__
+// Every launcher goes through mi_launch.  grid == 0 launches nothing: it
+// resolves the instantiation on the current device (hipFuncGetAttributes
+// loads the code object that holds it), so mi_cls_ctx_create can load every
+// kernel of the library before the first launch and no code object is ever
+// first loaded later in the process's life (e.g. after specialised modules
+// were loaded).
+static inline const void *mi_kaddr(void (*k)(KArgs))
+{
+	return reinterpret_cast<const void *>(k);
+}
+
+static inline int mi_launch(const void *k, unsigned grid, unsigned block, size_t dyn, hipStream_t st,
+			    const KArgs &a)
+{
+	if (grid == 0) {
+		hipFuncAttributes fa;
+		return hipFuncGetAttributes(&fa, k) == hipSuccess ? 0 : -EIO;
+	}
+	void *args[] = { (void *)&a };
+	return hipLaunchKernel(k, dim3(grid), dim3(block), args, dyn, st) == hipSuccess ? 0 : -EIO;
+}
 
 // Variant builds for A/B runs (odp_amd/_build.py, MI_CLS_ONLY): translation
 // units outside the selected set are compiled with MI_CLS_STUB, so their
 // launchers instantiate no kernel and fail with -ENOSYS.
 #ifdef MI_CLS_STUB
-#undef hipLaunchKernelGGL
-#define hipLaunchKernelGGL(...) return -ENOSYS
+#define MI_LAUNCH(K, grid, block, dyn, st, a) return -ENOSYS
+#else
+#define MI_LAUNCH(K, grid, block, dyn, st, a)                                             \
+	do {                                                                               \
+		const int rc_ = mi_launch(mi_kaddr(K), grid, (unsigned)(block), dyn, st, a); \
+		if (rc_)                                                                   \
+			return rc_;                                                        \
+	} while (0)
 #endif
+
+#endif   // !__HIPCC_RTC__

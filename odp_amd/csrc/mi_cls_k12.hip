@@ -6,8 +6,8 @@ int mi_cls_launch_k12(bool lt, bool div, unsigned grid, size_t dyn, hipStream_t 
 {
 	(void)lt;   // 12-wave blocks exist for LDS-resident hot regions only
 	if (div)
-		hipLaunchKernelGGL((mi_cls_kernel<true, true, 12>), dim3(grid), dim3(12 * WAVE), dyn, st, a);
+		MI_LAUNCH((mi_cls_kernel<true, true, 12>), grid, 12 * WAVE, dyn, st, a);
 	else
-		hipLaunchKernelGGL((mi_cls_kernel<true, false, 12>), dim3(grid), dim3(12 * WAVE), dyn, st, a);
+		MI_LAUNCH((mi_cls_kernel<true, false, 12>), grid, 12 * WAVE, dyn, st, a);
 	return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }

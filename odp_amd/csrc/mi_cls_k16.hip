@@ -5,12 +5,12 @@
 int mi_cls_launch_k16(bool lt, bool div, unsigned grid, size_t dyn, hipStream_t st, const KArgs &a)
 {
 	if (lt && div)
-		hipLaunchKernelGGL((mi_cls_kernel<true, true, 16>), dim3(grid), dim3(16 * WAVE), dyn, st, a);
+		MI_LAUNCH((mi_cls_kernel<true, true, 16>), grid, 16 * WAVE, dyn, st, a);
 	else if (lt)
-		hipLaunchKernelGGL((mi_cls_kernel<true, false, 16>), dim3(grid), dim3(16 * WAVE), dyn, st, a);
+		MI_LAUNCH((mi_cls_kernel<true, false, 16>), grid, 16 * WAVE, dyn, st, a);
 	else if (div)
-		hipLaunchKernelGGL((mi_cls_kernel<false, true, 16>), dim3(grid), dim3(16 * WAVE), dyn, st, a);
+		MI_LAUNCH((mi_cls_kernel<false, true, 16>), grid, 16 * WAVE, dyn, st, a);
 	else
-		hipLaunchKernelGGL((mi_cls_kernel<false, false, 16>), dim3(grid), dim3(16 * WAVE), dyn, st, a);
+		MI_LAUNCH((mi_cls_kernel<false, false, 16>), grid, 16 * WAVE, dyn, st, a);
 	return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }

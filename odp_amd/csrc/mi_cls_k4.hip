@@ -5,12 +5,12 @@
 int mi_cls_launch_k4(bool lt, bool div, unsigned grid, size_t dyn, hipStream_t st, const KArgs &a)
 {
 	if (lt && div)
-		hipLaunchKernelGGL((mi_cls_kernel<true, true, 4>), dim3(grid), dim3(4 * WAVE), dyn, st, a);
+		MI_LAUNCH((mi_cls_kernel<true, true, 4>), grid, 4 * WAVE, dyn, st, a);
 	else if (lt)
-		hipLaunchKernelGGL((mi_cls_kernel<true, false, 4>), dim3(grid), dim3(4 * WAVE), dyn, st, a);
+		MI_LAUNCH((mi_cls_kernel<true, false, 4>), grid, 4 * WAVE, dyn, st, a);
 	else if (div)
-		hipLaunchKernelGGL((mi_cls_kernel<false, true, 4>), dim3(grid), dim3(4 * WAVE), dyn, st, a);
+		MI_LAUNCH((mi_cls_kernel<false, true, 4>), grid, 4 * WAVE, dyn, st, a);
 	else
-		hipLaunchKernelGGL((mi_cls_kernel<false, false, 4>), dim3(grid), dim3(4 * WAVE), dyn, st, a);
+		MI_LAUNCH((mi_cls_kernel<false, false, 4>), grid, 4 * WAVE, dyn, st, a);
 	return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }

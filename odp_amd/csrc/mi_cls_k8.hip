@@ -6,8 +6,8 @@ int mi_cls_launch_k8(bool lt, bool div, unsigned grid, size_t dyn, hipStream_t s
 {
 	(void)lt;   // 8-wave blocks exist for LDS-resident hot regions only
 	if (div)
-		hipLaunchKernelGGL((mi_cls_kernel<true, true, 8>), dim3(grid), dim3(8 * WAVE), dyn, st, a);
+		MI_LAUNCH((mi_cls_kernel<true, true, 8>), grid, 8 * WAVE, dyn, st, a);
 	else
-		hipLaunchKernelGGL((mi_cls_kernel<true, false, 8>), dim3(grid), dim3(8 * WAVE), dyn, st, a);
+		MI_LAUNCH((mi_cls_kernel<true, false, 8>), grid, 8 * WAVE, dyn, st, a);
 	return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }

@@ -6,8 +6,8 @@
 int mi_cls_launch_ck16(bool div, unsigned grid, size_t dyn, hipStream_t st, const KArgs &a)
 {
 	if (div)
-		hipLaunchKernelGGL((mi_cls_kernel<true, true, 16, -1, true>), dim3(grid), dim3(16 * WAVE), dyn, st, a);
+		MI_LAUNCH((mi_cls_kernel<true, true, 16, -1, true>), grid, 16 * WAVE, dyn, st, a);
 	else
-		hipLaunchKernelGGL((mi_cls_kernel<true, false, 16, -1, true>), dim3(grid), dim3(16 * WAVE), dyn, st, a);
+		MI_LAUNCH((mi_cls_kernel<true, false, 16, -1, true>), grid, 16 * WAVE, dyn, st, a);
 	return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }

@@ -16,12 +16,12 @@ int mi_cls_launch_ck(int nw, bool lt, bool div, unsigned grid, size_t dyn, hipSt
 	if (nw != 4)
 		return -EINVAL;
 	if (lt && div)
-		hipLaunchKernelGGL((mi_cls_kernel<true, true, 4, -1, true>), dim3(grid), dim3(4 * WAVE), dyn, st, a);
+		MI_LAUNCH((mi_cls_kernel<true, true, 4, -1, true>), grid, 4 * WAVE, dyn, st, a);
 	else if (lt)
-		hipLaunchKernelGGL((mi_cls_kernel<true, false, 4, -1, true>), dim3(grid), dim3(4 * WAVE), dyn, st, a);
+		MI_LAUNCH((mi_cls_kernel<true, false, 4, -1, true>), grid, 4 * WAVE, dyn, st, a);
 	else if (div)
-		hipLaunchKernelGGL((mi_cls_kernel<false, true, 4, -1, true>), dim3(grid), dim3(4 * WAVE), dyn, st, a);
+		MI_LAUNCH((mi_cls_kernel<false, true, 4, -1, true>), grid, 4 * WAVE, dyn, st, a);
 	else
-		hipLaunchKernelGGL((mi_cls_kernel<false, false, 4, -1, true>), dim3(grid), dim3(4 * WAVE), dyn, st, a);
+		MI_LAUNCH((mi_cls_kernel<false, false, 4, -1, true>), grid, 4 * WAVE, dyn, st, a);
 	return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }

@@ -14,16 +14,16 @@ static int launch_fm(int fm, unsigned grid, size_t dyn, hipStream_t st, const KA
 {
 	switch (fm) {
 	case 0:
-		hipLaunchKernelGGL((mi_cls_kernel<true, false, NW, 0>), dim3(grid), dim3(NW * WAVE), dyn, st, a);
+		MI_LAUNCH((mi_cls_kernel<true, false, NW, 0>), grid, NW * WAVE, dyn, st, a);
 		break;
 	case 2:
-		hipLaunchKernelGGL((mi_cls_kernel<true, false, NW, 2>), dim3(grid), dim3(NW * WAVE), dyn, st, a);
+		MI_LAUNCH((mi_cls_kernel<true, false, NW, 2>), grid, NW * WAVE, dyn, st, a);
 		break;
 	case 3:
-		hipLaunchKernelGGL((mi_cls_kernel<true, false, NW, 3>), dim3(grid), dim3(NW * WAVE), dyn, st, a);
+		MI_LAUNCH((mi_cls_kernel<true, false, NW, 3>), grid, NW * WAVE, dyn, st, a);
 		break;
 	case 4:
-		hipLaunchKernelGGL((mi_cls_kernel<true, false, NW, 4>), dim3(grid), dim3(NW * WAVE), dyn, st, a);
+		MI_LAUNCH((mi_cls_kernel<true, false, NW, 4>), grid, NW * WAVE, dyn, st, a);
 		break;
 	default:
 		return -EINVAL;

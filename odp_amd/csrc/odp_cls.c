@@ -1417,6 +1417,16 @@ int odp_amd_cls_classify_host_wait(odp_pktio_t h, uint64_t ticket)
 	return e->ctx ? mi_cls_classify_host_wait(e->ctx, ticket) : -EINVAL;
 }
 
+/* Kernel instantiation of the pktio's last device launch (mi_cls_last_launch). */
+int odp_amd_cls_last_launch(odp_pktio_t h, uint32_t *info, uint32_t n)
+{
+	pktio_t *e = get_pktio(h);
+
+	if (!e || !e->ctx)
+		return -EINVAL;
+	return mi_cls_last_launch(e->ctx, info, n);
+}
+
 int odp_amd_cls_spec_wait(odp_pktio_t h)
 {
 	pktio_t *e = get_pktio(h);
