@@ -286,6 +286,20 @@ int mi_cls_group_classify_host(mi_cls_group_t *group, const uint8_t *pkts_host, 
 			       const uint32_t *off_host, const uint16_t *len_host, uint32_t n,
 			       mi_cls_result_t *out_host);
 
+/* Pipelined form of mi_cls_group_classify_host (the multi-GPU receive
+ * path's submit / wait, as mi_cls_classify_host_submit for one context):
+ * every device's slice is put in flight and a ticket returned;
+ * mi_cls_group_classify_host_wait(ticket) returns once all records are in
+ * out_host.  Batch, descriptors and records must be page-locked
+ * (mi_cls_host_alloc) to be read and written in place; otherwise the batch
+ * is classified synchronously and *ticket is 0 (done).  Up to 8 batches in
+ * flight, completed in submission order.  Replaces running the receive
+ * burst (pktio/loop.c:253-384) once per device, synchronously. */
+int mi_cls_group_classify_host_submit(mi_cls_group_t *group, const uint8_t *pkts_host, size_t bytes,
+				      const uint32_t *off_host, const uint16_t *len_host, uint32_t n,
+				      mi_cls_result_t *out_host, uint64_t *ticket);
+int mi_cls_group_classify_host_wait(mi_cls_group_t *group, uint64_t ticket);
+
 /* pktin parse options for the following classify calls on this context:
  * odp_pktin_config_opt_t.all_bits (include/odp_rt.h; reference
  * include/odp/api/spec/packet_io.h odp_pktin_config_opt_t).  Bits 2-5
@@ -296,6 +310,80 @@ int mi_cls_group_classify_host(mi_cls_group_t *group, const uint8_t *pkts_host, 
  * is the plain parse.  Replaces the `opt` argument of
  * _odp_packet_parse_common (include/odp_parse_internal.h:80-112). */
 int mi_cls_pktin_opt_set(mi_cls_ctx_t *ctx, uint64_t opt);
+
+/* ------------------------------------------------------------------------
+ * Receive delivery on the GPU: the host steps of loopback_recv /
+ * pcapif_recv_pkt after classification (pktio/loop.c:308-373, pcap.c:
+ * 330-352) for packets whose headers and buffers are in page-locked host
+ * memory the device addresses at the host's addresses: each packet's
+ * metadata (_odp_packet_parse_common's result at the pktio's parser layer,
+ * hdr->cos / cls_mark / dst_queue of _odp_cls_classify_packet, input pktio)
+ * written into its header, its frame copied into its buffer (pcap frames,
+ * pool switch, _odp_pktio_packet_to_pool), and the stable group-by-queue
+ * permutation of _odp_cls_enq's runs (include/odp_classification_internal.h:
+ * 208-236: each queue receives its packets in arrival order).
+ * ---------------------------------------------------------------------- */
+
+/* The receive-path fields of a packet header (the runtime's packet header
+ * embeds this block; odp_packet_hdr_t.p / cos / cls_mark / dst_queue /
+ * input, platform/linux-generic/include/odp_packet_internal.h:55-70,112-139). */
+typedef struct mi_cls_pkt_meta {
+	uint32_t data_off;      /* headroom                                        */
+	uint32_t len;
+	uint64_t in_flags;      /* packet_parser_t.input_flags                      */
+	uint8_t  err;           /* flags.all.error                                  */
+	uint8_t  cos;           /* 0xFF none                                        */
+	uint16_t cls_mark;
+	uint16_t l2, l3, l4;
+	uint16_t rsv0;
+	uint32_t rsv1;
+	uint64_t dst_queue;     /* odp_queue_t                                      */
+	uint64_t input;         /* odp_pktio_t                                      */
+	uint64_t user_ptr;
+	uint64_t rsv2;
+} mi_cls_pkt_meta_t;    /* 64 B: one cache line of the header, written whole */
+
+/* One delivered packet (host-written, 48 B). */
+typedef struct mi_cls_dlv {
+	uint64_t meta;          /* address of its mi_cls_pkt_meta_t (64-B aligned)   */
+	uint64_t dst_queue;     /* queue written into meta when the classifier is on */
+	uint64_t user_ptr;      /* kept user pointer (not MI_CLS_DLV_FRESH)          */
+	uint32_t src;           /* frame offset from the batch base (MI_CLS_DLV_COPY) */
+	uint32_t rec;           /* index of its record                              */
+	uint16_t len;           /* frame length                                     */
+	uint8_t  flags;         /* MI_CLS_DLV_*                                     */
+	uint8_t  qid;           /* queue group 0..MI_CLS_DLV_GROUPS-1, 0xFF none    */
+	uint32_t data_off;      /* the packet's headroom (kept: not MI_CLS_DLV_FRESH) */
+	uint64_t rsv;
+} mi_cls_dlv_t;
+
+#define MI_CLS_DLV_FRESH 0x01u  /* newly allocated: initialise every field     */
+#define MI_CLS_DLV_COPY  0x02u  /* copy the frame into meta + data_from_meta    */
+#define MI_CLS_DLV_CLS   0x04u  /* classifier on: cos / cls_mark / dst_queue    */
+#define MI_CLS_DLV_GROUPS 64
+
+typedef struct mi_cls_dlv_args {
+	const uint8_t *base;    /* the classified batch's base (host VA)           */
+	const mi_cls_result_t *res;   /* its records                              */
+	const mi_cls_dlv_t *dlv;
+	uint32_t n;             /* entries of dlv                                   */
+	uint32_t layer;         /* parser layer (ODP_PROTO_LAYER_L2..ALL = 1..4)    */
+	uint64_t input;         /* odp_pktio_t written into meta                    */
+	uint32_t headroom;      /* data_off of fresh packets                        */
+	uint32_t data_from_meta;/* bytes from a meta block to the packet's data     */
+	uint32_t *perm;         /* out: entry indexes grouped by qid (stable)       */
+	uint32_t *gcnt;         /* out: MI_CLS_DLV_GROUPS entry counts per qid       */
+} mi_cls_dlv_args_t;
+
+/* Submit the delivery of a classified burst on the context's stream (after
+ * its classification) and return a ticket for mi_cls_classify_host_wait.
+ * Every pointer is host memory the device reads and writes in place
+ * (mi_cls_host_alloc); entries with qid 0xFF are left out of perm. */
+int mi_cls_deliver_submit(mi_cls_ctx_t *ctx, const mi_cls_dlv_args_t *args, uint64_t *ticket);
+
+/* 1 if p lies in page-locked host memory that the device addresses at the
+ * same address (the receive delivery's requirement), else 0. */
+int mi_cls_host_mapped(const void *p);
 
 /* Pinned (page-locked) host memory for staging; NULL on failure. */
 void *mi_cls_host_alloc(size_t bytes);

@@ -311,6 +311,13 @@ int odp_amd_cls_spec_wait(odp_pktio_t pktio);
  * specialised, pktin-option kernel, grid). */
 int odp_amd_cls_last_launch(odp_pktio_t pktio, uint32_t *info, uint32_t n);
 
+/* GPU receive delivery of a classified burst on the pktio's device
+ * (mi_cls_deliver_submit; the runtime's receive path after classification,
+ * pktio/loop.c:308-373).  Wait with odp_amd_cls_deliver_wait. */
+struct mi_cls_dlv_args;
+int odp_amd_cls_deliver(odp_pktio_t pktio, const struct mi_cls_dlv_args *args, uint64_t *ticket);
+int odp_amd_cls_deliver_wait(odp_pktio_t pktio, uint64_t ticket);
+
 /* Create the device context, upload the current rule snapshot and run a
  * warm-up launch (odp_pktio_start). */
 int odp_amd_cls_prepare(odp_pktio_t pktio, int parse_only);

@@ -59,7 +59,7 @@ def build(force: bool = False, out_dir: str = PKG, defines=()) -> list[str]:
     built = []
     mi_hdr = os.path.join(SRC, "mi_cls_dev.h")
     k_srcs = [os.path.join(SRC, f"mi_cls_k{w}.hip") for w in (4, 8, 12, 16, "f", "f12", "f16", "c4",
-                                                              "c16")]
+                                                              "c16", "d")]
     if force or defines or _stale(mi_so, [mi_src, mi_hdr] + k_srcs + hdrs + [__file__]):
         # one translation unit per block shape + the host code, compiled in
         # parallel (the kernel instantiations dominate the build time)

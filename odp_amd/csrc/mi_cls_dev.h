@@ -2500,6 +2500,8 @@ int mi_cls_launch_flat(int nw, int fm, unsigned grid, size_t dyn, hipStream_t st
 // pktin-option kernels (CK; NW 4 or 16): mi_cls_kc.hip
 int mi_cls_launch_ck(int nw, bool lt, bool div, unsigned grid, size_t dyn, hipStream_t st,
 		     const KArgs &a);
+// receive delivery (mi_cls_kd.hip); grid 0: preload only
+int mi_cls_launch_deliver(unsigned grid, hipStream_t st, const mi_cls_dlv_args_t &h);
 
 // Every launcher goes through mi_launch.  grid == 0 launches nothing: it
 // resolves the instantiation on the current device (hipFuncGetAttributes

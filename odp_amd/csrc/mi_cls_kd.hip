@@ -1,0 +1,240 @@
+// mi_cls_kd.hip -- receive delivery on the GPU (mi_cls_deliver_submit).
+//
+// After a burst is classified, the host decides each frame's fate (parse
+// drop, CoS drop / discard, destination pool), takes the packets, and hands
+// the device one 32-B mi_cls_dlv_t per delivered packet.  This kernel then
+// does the per-packet host steps of loopback_recv / pcapif_recv_pkt that
+// follow classification (platform/linux-generic/pktio/loop.c:308-373,
+// pcap.c:330-352) straight into page-locked host memory:
+//   * the packet's receive metadata (packet_parse_reset + the parse result at
+//     the pktio's parser layer, hdr->cos / cls_mark / dst_queue of
+//     _odp_cls_classify_packet, odp_classification.c:1742-1771, hdr->input);
+//   * the frame copied into the packet's buffer (pcap frames, the pool switch
+//     of _odp_pktio_packet_to_pool, include/odp_packet_io_internal.h:352-371);
+//   * the stable group-by-queue permutation of the burst: _odp_cls_enq
+//     (include/odp_classification_internal.h:208-236) enqueues runs of equal
+//     (queue, CoS) in arrival order; grouping every packet of a queue in
+//     arrival order gives each queue the same sequence with one enqueue per
+//     queue.
+// One block of 256 threads serves 16 packets (16 lanes each: lane 0 the
+// metadata, all 16 the copy in 16-B pieces, 256 B per round); the last block
+// builds the permutation.  HBM is not involved: every byte moves over the
+// host link, so the kernel's bound is the link, not the chip.
+#include "mi_cls_dev.h"
+
+struct DArgs {
+	const uint8_t *base;
+	const mi_cls_result_t *res;
+	const mi_cls_dlv_t *dlv;
+	uint32_t n;
+	uint32_t layer;
+	uint64_t input;
+	uint32_t headroom;
+	uint32_t data_from_meta;
+	uint32_t *perm;
+	uint32_t *gcnt;
+};
+
+#define DLV_PER_BLOCK 16
+#define DLV_THREADS 256
+
+// apply_layer (odp_pktio.c): what a parser layer below L4 keeps of the full
+// parse (odp_parse.c:372-414)
+__device__ __forceinline__ void dlv_layer(uint32_t layer, uint32_t &fl, uint32_t &err, uint32_t &l4)
+{
+	const uint32_t L2F = (1u << 3) | (0x3fu << 6);
+	const uint32_t L3F = L2F | (1u << 4) | (0x7fu << 12);
+	if (layer >= 3u)   // ODP_PROTO_LAYER_L4 / ALL
+		return;
+	if (layer == 1u) {   // L2
+		fl &= L2F;
+		err &= 0x01u;
+		l4 = 0xFFFFu;
+	} else {             // L3
+		fl &= L3F | (1u << 30);
+		err &= 0x07u;
+	}
+}
+
+// The last block: the stable permutation of the entries with qid < 64,
+// grouped by qid.  The entries' qids are read once into LDS (every load in
+// flight at once: the entries are in host memory), then counted, and each
+// entry's place = its group's start + the entries of its group before it:
+// per 256-entry chunk a ballot loop over each wave's distinct qids gives the
+// rank inside the wave, the other waves' counts the rest.  Bursts of more
+// than DLV_GROUP_MAX entries are not grouped (the host leaves qid 0xFF).
+#define DLV_GROUP_MAX 8192
+__device__ void dlv_group(const DArgs &a)
+{
+	__shared__ uint8_t s_q[DLV_GROUP_MAX];
+	__shared__ uint32_t s_cnt[MI_CLS_DLV_GROUPS];
+	__shared__ uint32_t s_pos[MI_CLS_DLV_GROUPS];
+	__shared__ uint32_t s_w[DLV_THREADS / WAVE][MI_CLS_DLV_GROUPS];
+	const uint32_t t = threadIdx.x, lane = t & (WAVE - 1), wave = t / WAVE;
+	const uint32_t n = a.n < DLV_GROUP_MAX ? a.n : DLV_GROUP_MAX;
+	if (t < MI_CLS_DLV_GROUPS)
+		s_cnt[t] = 0u;
+	{
+		// 32 qids per thread, loaded before any is used
+		uint8_t q[DLV_GROUP_MAX / DLV_THREADS];
+#pragma unroll
+		for (uint32_t k = 0; k < DLV_GROUP_MAX / DLV_THREADS; ++k) {
+			const uint32_t i = t + k * DLV_THREADS;
+			q[k] = i < n ? a.dlv[i].qid : (uint8_t)0xFFu;
+		}
+#pragma unroll
+		for (uint32_t k = 0; k < DLV_GROUP_MAX / DLV_THREADS; ++k)
+			s_q[t + k * DLV_THREADS] = q[k];
+	}
+	__syncthreads();
+	for (uint32_t i = t; i < n; i += DLV_THREADS)
+		if (s_q[i] < MI_CLS_DLV_GROUPS)
+			atomicAdd(&s_cnt[s_q[i]], 1u);
+	__syncthreads();
+	if (t == 0) {
+		uint32_t at = 0;
+		for (uint32_t g = 0; g < MI_CLS_DLV_GROUPS; ++g) {
+			s_pos[g] = at;
+			at += s_cnt[g];
+		}
+	}
+	if (t < MI_CLS_DLV_GROUPS)
+		a.gcnt[t] = s_cnt[t];
+	__syncthreads();
+	const unsigned long long lt = lane ? (~0ull >> (64u - lane)) : 0ull;
+	for (uint32_t c0 = 0; c0 < n; c0 += DLV_THREADS) {
+		const uint32_t i = c0 + t;
+		const uint32_t q = i < n ? s_q[i] : 0xFFu;
+		bool left = q < MI_CLS_DLV_GROUPS;
+		uint32_t rank = 0;
+		for (uint32_t g = lane; g < MI_CLS_DLV_GROUPS; g += WAVE)
+			s_w[wave][g] = 0u;
+		__syncthreads();
+		for (;;) {
+			const unsigned long long m = __ballot(left);
+			if (!m)
+				break;
+			const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)q, (int)__builtin_ctzll(m));
+			const unsigned long long mv = __ballot(left && q == v);
+			if (left && q == v) {
+				rank = (uint32_t)__popcll(mv & lt);
+				left = false;
+			}
+			if (lane == 0)
+				s_w[wave][v] = (uint32_t)__popcll(mv);
+		}
+		__syncthreads();
+		if (q < MI_CLS_DLV_GROUPS) {
+			uint32_t before = 0;
+			for (uint32_t w = 0; w < wave; ++w)
+				before += s_w[w][q];
+			a.perm[s_pos[q] + before + rank] = i;
+		}
+		__syncthreads();
+		if (t < MI_CLS_DLV_GROUPS) {
+			uint32_t all = 0;
+			for (uint32_t w = 0; w < DLV_THREADS / WAVE; ++w)
+				all += s_w[w][t];
+			s_pos[t] += all;
+		}
+		__syncthreads();
+	}
+}
+
+// One packet's metadata block (64 B, one cache line of its header): four
+// 16-B stores by lanes 0-3 of its 16-lane group, so the line crosses the
+// host link as one full write (no read-modify-write at the host, and the
+// header line the pool and queues use is not touched).
+__global__ __launch_bounds__(DLV_THREADS) void mi_cls_deliver_kernel(DArgs a)
+{
+	if (blockIdx.x == gridDim.x - 1) {
+		dlv_group(a);
+		return;
+	}
+	const uint32_t sub = threadIdx.x & 15u;
+	const uint32_t j = blockIdx.x * DLV_PER_BLOCK + (threadIdx.x >> 4);
+	if (j >= a.n)
+		return;
+	const mi_cls_dlv_t d = a.dlv[j];
+	uint8_t *meta = (uint8_t *)(uintptr_t)d.meta;
+	if (sub < 4u) {
+		const mi_cls_result_t r = a.res[d.rec];
+		uint32_t fl = r.in_flags, err = r.err, l4 = r.l4_offset;
+		dlv_layer(a.layer, fl, err, l4);
+		const bool cls = (d.flags & MI_CLS_DLV_CLS) != 0u;
+		const bool fresh = (d.flags & MI_CLS_DLV_FRESH) != 0u;
+		uint32_t cos = 0xFFu, mark = 0u;
+		uint64_t dq = 0u;
+		if (cls) {
+			cos = r.cos;
+			mark = r.mark;
+			dq = d.dst_queue;
+		} else if (!fresh) {
+			// parser-only pktio, packet received as it was sent: its
+			// classification fields stay
+			const mi_cls_pkt_meta_t *m = (const mi_cls_pkt_meta_t *)meta;
+			cos = m->cos;
+			mark = m->cls_mark;
+			dq = m->dst_queue;
+		}
+		const uint64_t up = fresh ? 0u : d.user_ptr;
+		u32x4 v;
+		if (sub == 0u) {
+			// data_off, len, in_flags (bits 32-63 are never set on this path)
+			v = u32x4{ fresh ? a.headroom : d.data_off, d.len, fl, 0u };
+		} else if (sub == 1u) {
+			// err, cos, cls_mark | l2, l3 | l4, rsv0 | rsv1
+			v = u32x4{ err | (cos << 8) | (mark << 16), (uint32_t)r.l3_offset << 16, l4, 0u };
+		} else if (sub == 2u) {
+			v = u32x4{ (uint32_t)dq, (uint32_t)(dq >> 32), (uint32_t)a.input,
+				   (uint32_t)(a.input >> 32) };
+		} else {
+			v = u32x4{ (uint32_t)up, (uint32_t)(up >> 32), 0u, 0u };
+		}
+		((u32x4 *)meta)[sub] = v;
+	}
+	if (d.flags & MI_CLS_DLV_COPY) {
+		// the frame in rounds of 1536 B: each lane's six 16-B loads are all
+		// issued before its stores (host-memory reads: a latency each)
+		const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+			(void *)a.base, (short)0, (int)OOB_OFF, 0x00020000);
+		u32x4 *dst = (u32x4 *)(meta + a.data_from_meta);
+		for (uint32_t o0 = 16u * sub; o0 < d.len; o0 += 6u * 256u) {
+			u32x4 v[6];
+#pragma unroll
+			for (uint32_t k = 0; k < 6; ++k) {
+				const uint32_t o = o0 + 256u * k;
+				v[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, o < d.len ? d.src + o : OOB_OFF, 0, 0);
+			}
+#pragma unroll
+			for (uint32_t k = 0; k < 6; ++k) {
+				const uint32_t o = o0 + 256u * k;
+				if (o < d.len)
+					dst[o >> 4] = v[k];
+			}
+		}
+	}
+}
+
+int mi_cls_launch_deliver(unsigned grid, hipStream_t st, const mi_cls_dlv_args_t &h)
+{
+	DArgs a;
+	a.base = h.base;
+	a.res = h.res;
+	a.dlv = h.dlv;
+	a.n = h.n;
+	a.layer = h.layer;
+	a.input = h.input;
+	a.headroom = h.headroom;
+	a.data_from_meta = h.data_from_meta;
+	a.perm = h.perm;
+	a.gcnt = h.gcnt;
+	if (grid == 0) {   // preload (mi_cls_ctx_create)
+		hipFuncAttributes fa;
+		return hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(&mi_cls_deliver_kernel)) ==
+		       hipSuccess ? 0 : -EIO;
+	}
+	void *args[] = { &a };
+	return hipLaunchKernel(reinterpret_cast<const void *>(&mi_cls_deliver_kernel), dim3(grid),
+			       dim3(DLV_THREADS), args, 0, st) == hipSuccess ? 0 : -EIO;
+}

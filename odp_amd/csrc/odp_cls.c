@@ -1397,9 +1397,11 @@ int odp_amd_cls_classify_host_submit(odp_pktio_t h, const uint8_t *pkts, size_t 
 	if (rc)
 		return rc;
 	if (e->grp) {
+		/* every device's slice in flight (page-locked bursts; pageable
+		 * ones complete here with ticket 0) */
 		mi_cls_group_pktin_opt_set(e->grp, e->pktin_opt);
-		return mi_cls_group_classify_host(e->grp, pkts, bytes, off, len, n,
-						  (mi_cls_result_t *)out);
+		return mi_cls_group_classify_host_submit(e->grp, pkts, bytes, off, len, n,
+							 (mi_cls_result_t *)out, ticket);
 	}
 	mi_cls_pktin_opt_set(e->ctx, e->pktin_opt);
 	return mi_cls_classify_host_submit(e->ctx, pkts, bytes, off, len, n,
@@ -1414,7 +1416,36 @@ int odp_amd_cls_classify_host_wait(odp_pktio_t h, uint64_t ticket)
 		return -EINVAL;
 	if (ticket == 0)
 		return 0;
+	if (e->grp)
+		return mi_cls_group_classify_host_wait(e->grp, ticket);
 	return e->ctx ? mi_cls_classify_host_wait(e->ctx, ticket) : -EINVAL;
+}
+
+/* GPU receive delivery of a classified burst (mi_cls_deliver_submit) on the
+ * pktio's (first) device; waited for with odp_amd_cls_classify_host_wait. */
+int odp_amd_cls_deliver(odp_pktio_t h, const mi_cls_dlv_args_t *args, uint64_t *ticket)
+{
+	pktio_t *e = get_pktio(h);
+	int rc;
+
+	if (!e || !ticket)
+		return -EINVAL;
+	*ticket = 0;
+	rc = ensure_ctx(e);
+	if (rc)
+		return rc;
+	return mi_cls_deliver_submit(e->ctx, args, ticket);
+}
+
+/* Wait for a delivery ticket (the first device's ring, also for pktios over
+ * several devices, whose classify tickets belong to the group). */
+int odp_amd_cls_deliver_wait(odp_pktio_t h, uint64_t ticket)
+{
+	pktio_t *e = get_pktio(h);
+
+	if (!e || !e->ctx)
+		return -EINVAL;
+	return ticket ? mi_cls_classify_host_wait(e->ctx, ticket) : 0;
 }
 
 /* Kernel instantiation of the pktio's last device launch (mi_cls_last_launch). */

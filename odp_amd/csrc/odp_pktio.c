@@ -57,7 +57,18 @@ enum { DRV_LOOP = 1, DRV_PCAP, DRV_NULL };
 enum { ST_OPENED = 0, ST_STARTED, ST_STOPPED };
 
 #define RX_BURST_DEFAULT 4096
+/* staging sets per pktio: one burst staged and classified, one whose GPU
+ * delivery is in flight, one being staged */
+#define RX_SETS 3
+/* in-place loop bursts: offsets from the pinned arena's base stay below the
+ * kernel's out-of-range offset */
+#define OOB_SPAN ((size_t)0xF0000000u)
 #define PCAP_MTU_MAX (64 * 1024)
+
+/* Per-chunk pktio counters of a delivery. */
+typedef struct {
+	uint64_t in_errors, in_discards, octets, packets;
+} rx_cnt_t;
 
 /* One receive burst on its way through the GPU. */
 typedef struct {
@@ -74,6 +85,25 @@ typedef struct {
 	uint32_t tmp_cap;
 	uint32_t n_cap;
 	int arr_pinned;
+	/* GPU delivery (mi_cls_deliver_submit): entries, permutation and
+	 * group counts in page-locked memory; the packet of each entry */
+	mi_cls_dlv_t *dlv;
+	uint32_t *perm;
+	uint32_t *gcnt;
+	odp_packet_t *ent;      /* delivered packet per entry */
+	odp_packet_t *old;      /* loop packets whose frames the GPU copies out (pool switch) */
+	uint8_t *ppool;         /* loop: each packet's pool index + 1 (read at staging) */
+	uint16_t *pdoff;        /* loop: each packet's headroom */
+	const void **pup;       /* loop: each packet's user pointer */
+	int dlv_pinned;
+	/* a GPU delivery in flight (rx_dlv_start .. rx_dlv_end) */
+	int delivering;
+	uint64_t dticket;
+	int derr;               /* the submit failed */
+	uint32_t ne;            /* entries */
+	int nold, grouped, ng;
+	odp_queue_t gq[MI_CLS_DLV_GROUPS];
+	rx_cnt_t cnt;
 	int n;
 	int pending;            /* staged (and submitted), not delivered */
 	uint64_t ticket;        /* odp_amd_cls_classify_host_submit, 0 = done */
@@ -112,16 +142,19 @@ typedef struct {
 	int fbuf_pinned;        /* page-locked: the GPU reads frames in place */
 	/* GPU bursts: two staging sets, so one burst is classified while the
 	 * previous one is delivered (pipelined receive) */
-	rx_set_t rs[2];
+	rx_set_t rs[RX_SETS];
 	int cur;                /* set the next burst is staged into */
-	uint64_t prof[8];       /* ODP_AMD_RX_PROF: ns staging / classifying / delivering, bursts,
+	uint64_t prof[12];      /* ODP_AMD_RX_PROF: ns staging / classifying / delivering, bursts,
 				 * then of delivering: ns preparing / enqueueing, TSC ticks in
-				 * packet allocation / frame copies */
+				 * packet allocation / frame copies; GPU delivery: ns deciding +
+				 * taking packets + entries, ns in the delivery kernel (submit to
+				 * wait), ns enqueueing, bursts */
 } rt_pktio_t;
 
 static void rx_sets_free(rt_pktio_t *e);
 static void fbuf_free(rt_pktio_t *e);
 static int rx_finish(rt_pktio_t *e, rx_set_t *s, odp_packet_t out[], int max_out);
+static int rx_dlv_end(rt_pktio_t *e, rx_set_t *s, odp_packet_t out[], int max_out);
 
 static rt_pktio_t PK[RT_MAX_PKTIO];
 static odp_spinlock_t pk_lock;
@@ -765,10 +798,16 @@ int odp_pktio_stop(odp_pktio_t h)
 	}
 	sched_list_remove((int)((uintptr_t)h - 1));
 	odp_spinlock_lock(&e->rxl);   /* wait for an in-flight burst */
-	/* a burst still on the GPU was received before the stop: deliver it */
-	for (int k = 0; k < 2; k++)
-		if (e->rs[e->cur ^ 1 ^ k].pending)
-			(void)rx_finish(e, &e->rs[e->cur ^ 1 ^ k], NULL, 0);
+	/* bursts still on the GPU were received before the stop: deliver them,
+	 * oldest first */
+	for (int k = 1; k <= RX_SETS; k++) {
+		rx_set_t *s = &e->rs[(e->cur + k) % RX_SETS];
+
+		if (s->delivering)
+			(void)rx_dlv_end(e, s, NULL, 0);
+		if (s->pending)
+			(void)rx_finish(e, s, NULL, 0);
+	}
 	e->state = ST_STOPPED;
 	odp_spinlock_unlock(&e->rxl);
 	return 0;
@@ -787,8 +826,10 @@ int odp_pktio_close(odp_pktio_t h)
 	if (rx_prof > 0 && e->prof[3])
 		fprintf(stderr, "RXPROF %s bursts %" PRIu64 " stage_ns %" PRIu64 " classify_ns %" PRIu64
 			" deliver_ns %" PRIu64 " (prepare_ns %" PRIu64 " enqueue_ns %" PRIu64
-			" alloc_tsc %" PRIu64 " copy_tsc %" PRIu64 ")\n", e->name, e->prof[3], e->prof[0],
-			e->prof[1], e->prof[2], e->prof[4], e->prof[5], e->prof[6], e->prof[7]);
+			" alloc_tsc %" PRIu64 " copy_tsc %" PRIu64 ") gpu_bursts %" PRIu64
+			" (decide_ns %" PRIu64 " kernel_ns %" PRIu64 " enqueue_ns %" PRIu64 ")\n", e->name,
+			e->prof[3], e->prof[0], e->prof[1], e->prof[2], e->prof[4], e->prof[5], e->prof[6],
+			e->prof[7], e->prof[11], e->prof[8], e->prof[9], e->prof[10]);
 	if (e->inq != ODP_QUEUE_INVALID) {
 		odp_event_t ev[64];
 		int n;
@@ -848,6 +889,23 @@ static void rx_set_arrays_free(rx_set_t *s)
 	hmem_free(s->soff, s->arr_pinned);
 	hmem_free(s->slen, s->arr_pinned);
 	hmem_free(s->res, s->arr_pinned);
+	hmem_free(s->dlv, s->dlv_pinned);
+	hmem_free(s->perm, s->dlv_pinned);
+	hmem_free(s->gcnt, s->dlv_pinned);
+	free(s->ent);
+	free(s->old);
+	free(s->ppool);
+	free(s->pdoff);
+	free(s->pup);
+	s->pup = NULL;
+	s->dlv = NULL;
+	s->perm = NULL;
+	s->gcnt = NULL;
+	s->ent = NULL;
+	s->old = NULL;
+	s->ppool = NULL;
+	s->pdoff = NULL;
+	s->dlv_pinned = 0;
 	free(s->pk);
 	free(s->tmp);
 	s->tmp = NULL;
@@ -861,7 +919,7 @@ static void rx_set_arrays_free(rx_set_t *s)
 
 static void rx_sets_free(rt_pktio_t *e)
 {
-	for (int k = 0; k < 2; k++) {
+	for (int k = 0; k < RX_SETS; k++) {
 		rx_set_t *s = &e->rs[k];
 
 		hmem_free(s->stage, s->stage_pinned);
@@ -895,6 +953,34 @@ static int stage_reserve(rx_set_t *s, uint32_t n, size_t bytes)
 		if (!s->soff || !s->slen || !s->res || !s->pk) {
 			rx_set_arrays_free(s);
 			return -1;
+		}
+		/* GPU delivery arrays: only when all three are page-locked */
+		int q1, q2, q3;
+
+		s->dlv = hmem_alloc(c * sizeof(mi_cls_dlv_t), &q1);
+		s->perm = hmem_alloc(c * sizeof(uint32_t), &q2);
+		s->gcnt = hmem_alloc(MI_CLS_DLV_GROUPS * sizeof(uint32_t), &q3);
+		s->ent = malloc(c * sizeof(odp_packet_t));
+		s->old = malloc(c * sizeof(odp_packet_t));
+		s->ppool = malloc(c);
+		s->pdoff = malloc(c * sizeof(uint16_t));
+		s->pup = malloc(c * sizeof(void *));
+		if (!s->ppool || !s->pdoff || !s->pup) {
+			rx_set_arrays_free(s);
+			return -1;
+		}
+		s->dlv_pinned = q1 && q2 && q3 && s->dlv && s->perm && s->gcnt && s->ent && s->old;
+		if (!s->dlv_pinned) {
+			hmem_free(s->dlv, q1);
+			hmem_free(s->perm, q2);
+			hmem_free(s->gcnt, q3);
+			free(s->ent);
+			free(s->old);
+			s->dlv = NULL;
+			s->perm = NULL;
+			s->gcnt = NULL;
+			s->ent = NULL;
+			s->old = NULL;
 		}
 		s->n_cap = c;
 	}
@@ -1110,36 +1196,74 @@ static int stage_frames(rt_pktio_t *e, rx_set_t *s, uint32_t max)
 		}
 		s->bytes = in_place ? e->fbuf_bytes : off + 64;
 	} else if (e->drv == DRV_LOOP) {
-		odp_event_t ev[256];
+		/* Packets of page-locked pools are classified in place: the
+		 * descriptors are their data addresses relative to the lowest
+		 * pinned pool (one base for the burst; the GPU addresses that
+		 * memory at the host's addresses).  A burst with a packet outside
+		 * that range is copied into the stage instead. */
+		uint8_t *lo = NULL;
+		size_t span = 0;
+		int in_place = s->arr_pinned && rt_pinned_arena(&lo, &span) && span < OOB_SPAN;
+		uint8_t pinned_of[RT_MAX_POOLS];
+
+		for (int k = 0; k < RT_MAX_POOLS; k++) {
+			rt_pool_t *rp = rt_pool((odp_pool_t)(uintptr_t)(k + 1));
+
+			pinned_of[k] = rp && rp->pinned;
+		}
 
 		while (n < max) {
-			int want = max - n < 256 ? (int)(max - n) : 256;
+			odp_event_t *ev = (odp_event_t *)(void *)(s->pk + n);
+			int want = (int)(max - n);
 			int got = rt_queue_deq_multi_raw((rt_queue_t *)(void *)e->loopq, ev, want);
 
 			if (got <= 0)
 				break;
 			for (int i = 0; i < got; i++) {
+				if (i + 16 < got) {   /* both header lines (the sender wrote them) */
+					const uint8_t *nh = (const uint8_t *)rt_pkt_hdr(odp_packet_from_event(ev[i + 16]));
+
+					__builtin_prefetch(nh + 64);
+				}
 				odp_packet_t p = odp_packet_from_event(ev[i]);
 				pkt_hdr_t *h = rt_pkt_hdr(p);
+				const uint8_t *d = h->head + h->data_off;
 				uint32_t l = h->len > 65535 ? 65535 : h->len;
+				const uint32_t pi = h->ev.pool;
 
-				if (stage_reserve(s, max, off + l + 64)) {
-					odp_event_free_multi(&ev[i], got - i);
-					odp_packet_free_multi(s->pk, (int)n);
-					return -1;
-				}
-				memcpy(s->stage + off, h->head + h->data_off, l);
-				s->soff[n] = (uint32_t)off;
-				s->slen[n] = (uint16_t)l;
 				s->pk[n] = p;
-				off += (l + 63u) & ~63u;
+				s->slen[n] = (uint16_t)l;
+				s->ppool[n] = (uint8_t)(pi + 1u);
+				s->pdoff[n] = (uint16_t)h->data_off;
+				s->pup[n] = h->user_ptr;
+				if (in_place && pinned_of[pi] && d >= lo && (size_t)(d - lo) + l + 16u <= span)
+					s->soff[n] = (uint32_t)(d - lo);
+				else
+					in_place = 0;
 				n++;
 			}
 			if (got < want)
 				break;
 		}
-		s->base = s->stage;
-		s->bytes = off + 64;
+		if (in_place) {
+			s->base = lo;
+			s->bytes = span;
+		} else {
+			for (uint32_t i = 0; i < n; i++) {
+				pkt_hdr_t *h = rt_pkt_hdr(s->pk[i]);
+				const uint32_t l = s->slen[i];
+
+				if (stage_reserve(s, max, off + l + 64)) {
+					odp_packet_free_multi(s->pk, (int)n);
+					return -1;
+				}
+				memcpy(s->stage + off, h->head + h->data_off, l);
+				s->soff[i] = (uint32_t)off;
+				off += (l + 63u) & ~63u;
+			}
+			s->base = s->stage;
+			s->bytes = off + 64;
+		}
 	}
 	return (int)n;
 }
@@ -1201,11 +1325,6 @@ static int rx_classify(rt_pktio_t *e, rx_set_t *s, int pipe)
 	}
 	return 0;
 }
-
-/* Per-chunk pktio counters of a delivery. */
-typedef struct {
-	uint64_t in_errors, in_discards, octets, packets;
-} rx_cnt_t;
 
 /* The host steps of loopback_recv / pcapif_recv_pkt for frames [lo, hi) of
  * set s (loop.c:253-384, pcap.c:299-352; _odp_packet_parse_common's result
@@ -1622,58 +1741,377 @@ static void rx_enqueue(odp_packet_t pk[], int n, odp_packet_t *tmp, uint8_t *gid
 	}
 }
 
-/* Wait for set s's records and deliver its packets: classified ones to their
- * CoS queues, the rest (classifier disabled) into out[] (at most max_out).
- * Returns the packets placed in out[]. */
-static int rx_finish(rt_pktio_t *e, rx_set_t *s, odp_packet_t out[], int max_out)
+/* ODP_AMD_RX_GPU_DELIVER=0: host delivery only */
+static int gpu_deliver_on(void)
+{
+	static int on = -1;
+
+	if (on < 0) {
+		const char *v = getenv("ODP_AMD_RX_GPU_DELIVER");
+
+		on = !(v && v[0] == '0');
+	}
+	return on;
+}
+
+/* Enqueue the grouped packets of a GPU delivery: group g (queue gq[g]) holds
+ * entries perm[at .. at + gcnt[g]) in arrival order; queue statistics per
+ * CoS of the queue as per run of the reference. */
+static void rx_enqueue_groups(rx_set_t *s, const odp_queue_t *gq, int ng, odp_packet_t *tmp)
+{
+	uint32_t at = 0;
+
+	for (int g = 0; g < ng; g++) {
+		const uint32_t num = s->gcnt[g];
+		uint64_t ok[256], bad[256];
+		uint8_t seen[256];
+		int ncos = 0;
+		uint8_t cl[256];
+
+		if (!num)
+			continue;
+		for (uint32_t k = 0; k < num; k++)
+			tmp[k] = s->ent[s->perm[at + k]];
+		int r = odp_queue_enq_multi(gq[g], (const odp_event_t *)(void *)tmp, (int)num);
+
+		if (r < 0)
+			r = 0;
+		if ((uint32_t)r != num)
+			odp_packet_free_multi(&tmp[r], (int)num - r);
+		memset(seen, 0, sizeof(seen));
+		for (uint32_t k = 0; k < num; k++) {
+			const uint32_t cos = s->res[s->dlv[s->perm[at + k]].rec].cos;
+
+			if (!seen[cos]) {
+				seen[cos] = 1;
+				cl[ncos++] = (uint8_t)cos;
+				ok[cos] = 0;
+				bad[cos] = 0;
+			}
+			if (k < (uint32_t)r)
+				ok[cos]++;
+			else
+				bad[cos]++;
+		}
+		for (int k = 0; k < ncos; k++)
+			odp_amd_cls_queue_stats_add(cl[k], cos_slot_of(cl[k], gq[g]), ok[cl[k]],
+						    bad[cl[k]]);
+		at += num;
+	}
+}
+
+/* Delivery of set s on the GPU (mi_cls_deliver_submit): the host decides
+ * every frame from its record (parse drop, CoS drop / discard, destination
+ * pool: the same decisions and counters as rx_prepare), takes the packets
+ * from each pool at once, and hands the GPU one entry per delivered packet;
+ * the GPU writes the packets' metadata, copies frames that change buffers
+ * (pcap frames, loop packets switching pools) and groups the packets by
+ * queue; the host then enqueues each queue's packets with one call.  The
+ * host touches no packet header or frame byte on this path.  This starts
+ * it: the decisions, the packets, the entries, the kernel submitted (the set
+ * is then `delivering` until rx_dlv_end).  Returns 0, or -1 when the burst
+ * needs the host path (a destination pool not page-locked, more than
+ * RX_MAX_POOLS pools, frames the GPU cannot address) -- nothing has been
+ * done then. */
+static int rx_dlv_start(rt_pktio_t *e, rx_set_t *s, rx_cnt_t *c)
 {
 	const odp_proto_layer_t layer = e->parse_layer;
-	uint64_t t1 = prof_ns();
+	uint8_t *slot = s->tmp ? (uint8_t *)(void *)(s->tmp + s->tmp_cap) : NULL;
+	odp_packet_t *got = s->tmp;
+	struct {
+		odp_pool_t pool;
+		uint32_t cap;
+		int cnt, base, have, used;
+	} pl[RX_MAX_POOLS];
+	int npl = 0;
+	enum { A_NONE = 0xff, A_INPLACE = 0xfe };   /* else: index of the pool */
 
-	if (s->ticket) {
-		int rc = odp_amd_cls_classify_host_wait(e->hdl, s->ticket);
+	if (!gpu_deliver_on() || !s->dlv_pinned || !slot || layer == ODP_PROTO_LAYER_NONE ||
+	    !mi_cls_host_mapped(s->base))
+		return -1;
+	const uint64_t td0 = prof_ns();
+	/* per-burst caches of the CoS lookups (pool, queue of slot 0) */
+	odp_pool_t cpool[256];
+	odp_queue_t cq0[256];
+	uint8_t cseen[256];
 
-		s->ticket = 0;
+	memset(cseen, 0, sizeof(cseen));
+#define COS_SEEN(cos)                                                                  \
+	do {                                                                           \
+		if (!cseen[cos]) {                                                     \
+			cseen[cos] = 1;                                                \
+			cpool[cos] = odp_amd_cls_pool_of(cos);                         \
+			cq0[cos] = odp_amd_cls_queue_of(cos, 0);                       \
+		}                                                                      \
+	} while (0)
+	/* pass 1: the decision per frame, no side effects yet */
+	for (int i = 0; i < s->n; i++) {
+		mi_cls_result_t r = s->res[i];
+		odp_pool_t pool = e->pool;
+
+		if (i + 16 < s->n)
+			__builtin_prefetch(&s->res[i + 16]);
+		slot[i] = A_NONE;
+		apply_layer(&r, layer);
+		if (r.outcome == MI_CLS_OUT_PARSE_DROP)
+			continue;
+		if (e->cls_enabled) {
+			if (r.outcome != MI_CLS_OUT_ENQ)
+				continue;
+			COS_SEEN(r.cos);
+			if (cpool[r.cos] != ODP_POOL_INVALID)
+				pool = cpool[r.cos];
+		}
+		if (e->drv == DRV_LOOP && (odp_pool_t)(uintptr_t)s->ppool[i] == pool) {
+			/* the GPU writes the packet's own header */
+			if (!rt_pool(pool)->pinned)
+				return -1;
+			slot[i] = A_INPLACE;
+			continue;
+		}
+		int k = 0;
+
+		while (k < npl && pl[k].pool != pool)
+			k++;
+		if (k == npl) {
+			rt_pool_t *rp = rt_pool(pool);
+
+			if (npl == RX_MAX_POOLS || !rp || !rp->pinned)
+				return -1;
+			pl[k].pool = pool;
+			pl[k].cap = rp->param.type == ODP_POOL_PACKET ? rp->data_cap : 0u;
+			pl[k].cnt = 0;
+			npl++;
+		}
+		if (s->slen[i] > pl[k].cap)   /* odp_packet_alloc fails: discarded */
+			continue;
+		slot[i] = (uint8_t)k;
+		pl[k].cnt++;
+	}
+	/* pass 2: each pool's packets at once */
+	int at = 0;
+
+	for (int k = 0; k < npl; k++) {
+		pl[k].base = at;
+		pl[k].have = pl[k].cnt ? rt_packet_alloc_raw(pl[k].pool, 0, &got[at], pl[k].cnt) : 0;
+		pl[k].used = 0;
+		at += pl[k].cnt;
+	}
+	/* pass 3: counters, drops, entries (queue groups: every plain-enqueue
+	 * queue of the burst, at most MI_CLS_DLV_GROUPS) */
+	odp_queue_t gq[MI_CLS_DLV_GROUPS];
+	int ng = 0, grouped = e->cls_enabled, nold = 0;
+	int8_t mode_of_cos[256];
+	uint8_t slot_grp[RX_GROUP_HASH];
+	uint32_t ne = 0;
+
+	memset(mode_of_cos, -1, sizeof(mode_of_cos));
+	memset(slot_grp, 0, sizeof(slot_grp));
+	for (int i = 0; i < s->n; i++) {
+		mi_cls_result_t r = s->res[i];
+		const uint32_t len = s->slen[i];
+		const int k = slot[i];
+		odp_packet_t pkt = e->drv == DRV_LOOP ? s->pk[i] : ODP_PACKET_INVALID;
+
+		s->pk[i] = ODP_PACKET_INVALID;
+		apply_layer(&r, layer);
+		if (r.err || r.outcome == MI_CLS_OUT_PARSE_DROP)
+			c->in_errors++;
+		if (r.outcome == MI_CLS_OUT_PARSE_DROP) {
+			odp_packet_free(pkt);
+			continue;
+		}
+		if (e->cls_enabled && (r.outcome == MI_CLS_OUT_DISCARD || r.outcome == MI_CLS_OUT_LOOP))
+			c->in_discards++;
+		if (e->cls_enabled && r.outcome != MI_CLS_OUT_ENQ) {
+			odp_packet_free(pkt);
+			continue;
+		}
+		uint8_t fl = MI_CLS_DLV_FRESH | MI_CLS_DLV_COPY;
+		odp_packet_t dst;
+
+		if (k == A_INPLACE) {
+			dst = pkt;
+			fl = 0;
+		} else if (k == A_NONE || pl[k].used >= pl[k].have) {
+			/* too long for the pool, or the pool ran short (a loop
+			 * packet's failed pool switch is a discard either way) */
+			if (k != A_NONE)
+				pl[k].used++;
+			if (e->cls_enabled || pkt != ODP_PACKET_INVALID)
+				c->in_discards++;
+			odp_packet_free(pkt);
+			continue;
+		} else {
+			dst = got[pl[k].base + pl[k].used++];
+			if (pkt != ODP_PACKET_INVALID)
+				s->old[nold++] = pkt;   /* freed once the GPU copied it */
+		}
+		if (!r.err) {
+			c->octets += len;
+			c->packets++;
+		}
+		mi_cls_dlv_t *d = &s->dlv[ne];
+		uint8_t qid = 0xff;
+
+		d->meta = (uint64_t)(uintptr_t)&rt_pkt_hdr(dst)->meta;
+		d->data_off = k == A_INPLACE ? s->pdoff[i] : RT_PKT_HEADROOM;
+		/* the metadata line is written whole: a packet received in place
+		 * keeps its user pointer (read with its headroom at staging) */
+		d->user_ptr = k == A_INPLACE ? (uint64_t)(uintptr_t)s->pup[i] : 0u;
+		d->dst_queue = 0;
+		d->src = s->soff[i];
+		d->rec = (uint32_t)i;
+		d->len = (uint16_t)len;
+		if (e->cls_enabled) {
+			const odp_queue_t q = r.queue == 0 ? cq0[r.cos] : odp_amd_cls_queue_of(r.cos, r.queue);
+
+			fl |= MI_CLS_DLV_CLS;
+			d->dst_queue = (uint64_t)(uintptr_t)q;
+			if (grouped && mode_of_cos[r.cos] < 0) {
+				odp_pool_t vp = ODP_POOL_INVALID;
+				uint32_t vmax = 0;
+				int aggr = 0;
+				const int std = odp_amd_cls_cos_enq_mode(r.cos, &vp, &vmax, &aggr);
+
+				mode_of_cos[r.cos] = std > 0 && !aggr;
+			}
+			if (grouped && mode_of_cos[r.cos]) {
+				uint32_t sl = rx_qhash(q);
+
+				while (slot_grp[sl] && gq[slot_grp[sl] - 1] != q)
+					sl = (sl + 1) & (RX_GROUP_HASH - 1);
+				if (!slot_grp[sl]) {
+					if (ng == MI_CLS_DLV_GROUPS) {
+						grouped = 0;
+					} else {
+						gq[ng] = q;
+						slot_grp[sl] = (uint8_t)++ng;
+					}
+				}
+				if (grouped)
+					qid = (uint8_t)(slot_grp[sl] - 1);
+			} else {
+				grouped = 0;
+			}
+		}
+		d->flags = fl;
+		d->qid = qid;
+		s->ent[ne++] = dst;
+	}
+#undef COS_SEEN
+	/* the pools' packets nobody took back */
+	for (int k = 0; k < npl; k++)
+		if (pl[k].used < pl[k].have)
+			odp_packet_free_multi(&got[pl[k].base + pl[k].used], pl[k].have - pl[k].used);
+	if (!grouped)   /* per-run enqueue (vectors, aggregators, > 64 queues) */
+		for (uint32_t j = 0; j < ne; j++)
+			s->dlv[j].qid = 0xff;
+	s->ne = ne;
+	s->nold = nold;
+	s->grouped = grouped;
+	s->ng = ng;
+	memcpy(s->gq, gq, (size_t)ng * sizeof(odp_queue_t));
+	s->cnt = *c;
+	s->dticket = 0;
+	s->delivering = 1;
+	e->prof[8] += prof_ns() - td0;
+	e->prof[11]++;
+	if (ne) {
+		mi_cls_dlv_args_t a;
+
+		a.base = s->base;
+		a.res = s->res;
+		a.dlv = s->dlv;
+		a.n = ne;
+		a.layer = (uint32_t)layer;
+		a.input = (uint64_t)(uintptr_t)e->hdl;
+		a.headroom = RT_PKT_HEADROOM;
+		a.data_from_meta = rt_data_from_meta();
+		a.perm = s->perm;
+		a.gcnt = s->gcnt;
+		s->dticket = 0;
+		int rc = odp_amd_cls_deliver(e->hdl, &a, &s->dticket);
+
 		if (rc) {
-			rx_drop(e, s, rc);
-			return 0;
+			s->dticket = 0;
+			s->derr = rc;   /* rx_dlv_end drops the packets */
 		}
 	}
-	/* The control plane changed while the burst was in flight (a CoS
-	 * destroyed, its queues or pool changed, PMRs added or removed): its
-	 * records name CoS indexes of the old rule snapshot, so classify it again
-	 * under the current one -- what the synchronous path, which has no gap
-	 * between classify and enqueue, would deliver on this call. */
-	if (layer != ODP_PROTO_LAYER_NONE && e->cls_enabled && s->gen != odp_amd_cls_generation()) {
-		int rc = odp_amd_cls_classify_host(e->hdl, s->base, s->bytes, s->soff, s->slen,
-						   (uint32_t)s->n, s->res, 0);
+	return 0;
+}
 
-		if (rc) {
-			rx_drop(e, s, rc);
-			return 0;
+/* End the GPU delivery of set s (rx_dlv_start): wait for the kernel, give
+ * pool-switched packets their user pointers, enqueue (classifier on) or
+ * return the packets in out[] (at most max_out), add the counters.
+ * Returns the packets placed in out[]. */
+static int rx_dlv_end(rt_pktio_t *e, rx_set_t *s, odp_packet_t out[], int max_out)
+{
+	const uint64_t tk0 = prof_ns();
+	rx_cnt_t *c = &s->cnt;
+	int num_rx = 0, rc = s->derr;
+
+	if (!rc && s->dticket)
+		rc = odp_amd_cls_deliver_wait(e->hdl, s->dticket);
+	s->delivering = 0;
+	s->dticket = 0;
+	s->derr = 0;
+	if (rc) {
+		RT_ERR("pktio %s: GPU delivery failed (%s), %u packets dropped\n", e->name,
+		       mi_cls_strerror(rc), s->ne);
+		odp_packet_free_multi(s->ent, (int)s->ne);
+		odp_packet_free_multi(s->old, s->nold);
+		c->in_discards += s->ne;
+		s->ne = 0;
+		s->nold = 0;
+	}
+	/* pool switch: the new packet keeps the user pointer */
+	if (s->nold) {
+		int o = 0;
+
+		for (uint32_t j = 0; j < s->ne && o < s->nold; j++)
+			if (s->dlv[j].flags & MI_CLS_DLV_FRESH)
+				rt_pkt_hdr(s->ent[j])->user_ptr = rt_pkt_hdr(s->old[o++])->user_ptr;
+		odp_packet_free_multi(s->old, s->nold);
+		s->nold = 0;
+	}
+	const uint64_t tk1 = prof_ns();
+
+	if (!e->cls_enabled) {
+		for (uint32_t j = 0; j < s->ne; j++) {
+			if (num_rx < max_out)
+				out[num_rx++] = s->ent[j];
+			else
+				odp_packet_free(s->ent[j]);
 		}
+	} else if (s->grouped) {
+		rx_enqueue_groups(s, s->gq, s->ng, s->tmp);
+	} else if (s->ne) {
+		rx_enqueue(s->ent, (int)s->ne, s->tmp, (uint8_t *)(void *)(s->tmp + s->tmp_cap));
 	}
-	uint64_t t2 = prof_ns();
+	s->ne = 0;
+	e->prof[9] += tk1 - tk0;
+	e->prof[10] += prof_ns() - tk1;
+	if (c->in_errors)
+		odp_atomic_add_u64(&e->in_errors, c->in_errors);
+	if (c->in_discards)
+		odp_atomic_add_u64(&e->in_discards, c->in_discards);
+	odp_atomic_add_u64(&e->in_octets, c->octets);
+	odp_atomic_add_u64(&e->in_packets, c->packets);
+	return num_rx;
+}
 
-	e->prof[1] += t2 - t1;
-	s->pending = 0;
-	rx_cnt_t c;
+/* Delivery of set s on the host: rx_prepare, then the delivered packets,
+ * compacted in arrival order, to their queues or out[]. */
+static int rx_deliver_host(rt_pktio_t *e, rx_set_t *s, rx_cnt_t *c, odp_packet_t out[], int max_out,
+			   uint64_t t2)
+{
+	int nd = 0, num_rx = 0;
 
-	if (!s->tmp || s->tmp_cap < s->n_cap) {
-		/* delivery scratch: packets (bulk allocation, then grouping by
-		 * queue), then one byte per frame (its pool, then its queue group) */
-		free(s->tmp);
-		s->tmp = malloc(s->n_cap * (sizeof(odp_packet_t) + 1u));
-		s->tmp_cap = s->tmp ? s->n_cap : 0;
-	}
-	memset(&c, 0, sizeof(c));
-	rx_prepare(e, s, 0, s->n, &c);
+	rx_prepare(e, s, 0, s->n, c);
 	const uint64_t t3 = prof_ns();
 
 	e->prof[4] += t3 - t2;
-	/* the delivered packets, compacted in arrival order */
-	int nd = 0, num_rx = 0;
-
 	for (int i = 0; i < s->n; i++)
 		if (s->pk[i] != ODP_PACKET_INVALID)
 			s->pk[nd++] = s->pk[i];
@@ -1693,14 +2131,109 @@ static int rx_finish(rt_pktio_t *e, rx_set_t *s, odp_packet_t out[], int max_out
 		}
 	}
 	e->prof[5] += prof_ns() - t3;
-	e->prof[2] += prof_ns() - t2;
-	if (c.in_errors)
-		odp_atomic_add_u64(&e->in_errors, c.in_errors);
-	if (c.in_discards)
-		odp_atomic_add_u64(&e->in_discards, c.in_discards);
-	odp_atomic_add_u64(&e->in_octets, c.octets);
-	odp_atomic_add_u64(&e->in_packets, c.packets);
 	return num_rx;
+}
+
+/* Wait for set s's records and deliver its packets: classified ones to their
+ * CoS queues, the rest (classifier disabled) into out[] (at most max_out).
+ * Returns the packets placed in out[]. */
+/* Wait for set s's classification; a burst that was in flight while the
+ * control plane changed is classified again.  Returns 0, or -1 when the
+ * burst was dropped (rx_drop). */
+static int rx_classified(rt_pktio_t *e, rx_set_t *s)
+{
+	const odp_proto_layer_t layer = e->parse_layer;
+	uint64_t t1 = prof_ns();
+
+	if (s->ticket) {
+		int rc = odp_amd_cls_classify_host_wait(e->hdl, s->ticket);
+
+		s->ticket = 0;
+		if (rc) {
+			rx_drop(e, s, rc);
+			return -1;
+		}
+	}
+	/* The control plane changed while the burst was in flight (a CoS
+	 * destroyed, its queues or pool changed, PMRs added or removed): its
+	 * records name CoS indexes of the old rule snapshot, so classify it again
+	 * under the current one -- what the synchronous path, which has no gap
+	 * between classify and enqueue, would deliver on this call. */
+	if (layer != ODP_PROTO_LAYER_NONE && e->cls_enabled && s->gen != odp_amd_cls_generation()) {
+		int rc = odp_amd_cls_classify_host(e->hdl, s->base, s->bytes, s->soff, s->slen,
+						   (uint32_t)s->n, s->res, 0);
+
+		if (rc) {
+			rx_drop(e, s, rc);
+			return -1;
+		}
+	}
+	e->prof[1] += prof_ns() - t1;
+	s->pending = 0;
+	if (!s->tmp || s->tmp_cap < s->n_cap) {
+		/* delivery scratch: packets (bulk allocation, then grouping by
+		 * queue), then one byte per frame (its pool, then its queue group) */
+		free(s->tmp);
+		s->tmp = malloc(s->n_cap * (sizeof(odp_packet_t) + 1u));
+		s->tmp_cap = s->tmp ? s->n_cap : 0;
+	}
+	return 0;
+}
+
+/* Deliver set s on the host (the burst needs the host path). */
+static int rx_finish_host(rt_pktio_t *e, rx_set_t *s, rx_cnt_t *c, odp_packet_t out[], int max_out,
+			  uint64_t t2)
+{
+	const int num_rx = rx_deliver_host(e, s, c, out, max_out, t2);
+
+	e->prof[2] += prof_ns() - t2;
+	if (c->in_errors)
+		odp_atomic_add_u64(&e->in_errors, c->in_errors);
+	if (c->in_discards)
+		odp_atomic_add_u64(&e->in_discards, c->in_discards);
+	odp_atomic_add_u64(&e->in_octets, c->octets);
+	odp_atomic_add_u64(&e->in_packets, c->packets);
+	return num_rx;
+}
+
+/* Wait for set s's records and deliver its packets now: classified ones to
+ * their CoS queues, the rest (classifier disabled) into out[] (at most
+ * max_out).  Returns the packets placed in out[]. */
+static int rx_finish(rt_pktio_t *e, rx_set_t *s, odp_packet_t out[], int max_out)
+{
+	rx_cnt_t c;
+
+	if (rx_classified(e, s))
+		return 0;
+	const uint64_t t2 = prof_ns();
+
+	memset(&c, 0, sizeof(c));
+	if (rx_dlv_start(e, s, &c) == 0) {
+		const int num_rx = rx_dlv_end(e, s, out, max_out);
+
+		e->prof[2] += prof_ns() - t2;
+		return num_rx;
+	}
+	return rx_finish_host(e, s, &c, out, max_out, t2);
+}
+
+/* Classifier on: wait for set s's records and start its GPU delivery,
+ * leaving it in flight (rx_dlv_end on a later call); a burst that needs the
+ * host path is delivered now. */
+static void rx_finish_start(rt_pktio_t *e, rx_set_t *s)
+{
+	rx_cnt_t c;
+
+	if (rx_classified(e, s))
+		return;
+	const uint64_t t2 = prof_ns();
+
+	memset(&c, 0, sizeof(c));
+	if (rx_dlv_start(e, s, &c) == 0) {
+		e->prof[2] += prof_ns() - t2;
+		return;
+	}
+	(void)rx_finish_host(e, s, &c, NULL, 0, t2);
 }
 
 /* One receive call.  With the classifier enabled, a burst whose successor is
@@ -1711,7 +2244,11 @@ static int rx_finish(rt_pktio_t *e, rx_set_t *s, odp_packet_t out[], int max_out
  * ones are enqueued to their CoS queues. */
 static int pktio_recv(rt_pktio_t *e, odp_packet_t out[], int max_out)
 {
-	rx_set_t *s = &e->rs[e->cur], *p = &e->rs[e->cur ^ 1];
+	/* s: staged now; p: staged by the previous call (classified on the GPU
+	 * if it was left in flight); a: staged two calls ago (its GPU delivery
+	 * in flight if it was started) */
+	rx_set_t *s = &e->rs[e->cur], *p = &e->rs[(e->cur + RX_SETS - 1) % RX_SETS],
+		 *a = &e->rs[(e->cur + 1) % RX_SETS];
 	const int pipe = e->cls_enabled && e->parse_layer != ODP_PROTO_LAYER_NONE &&
 			 rx_pipeline();
 	uint32_t burst = rx_burst();
@@ -1739,7 +2276,7 @@ static int pktio_recv(rt_pktio_t *e, odp_packet_t out[], int max_out)
 	uint64_t t1 = prof_ns();
 
 	e->prof[0] += t1 - t0;
-	if (n < 0 && !p->pending)
+	if (n < 0 && !p->pending && !a->delivering)
 		return n;
 	s->n = n > 0 ? n : 0;
 	if (n > 0) {
@@ -1748,16 +2285,23 @@ static int pktio_recv(rt_pktio_t *e, odp_packet_t out[], int max_out)
 			n = 0;
 		e->prof[1] += prof_ns() - t1;
 	}
-	if (p->pending)
-		num_rx += rx_finish(e, p, out, max_out);
-	if (n > 0) {
-		/* only a burst really in flight waits (a multi-GPU pktio's submit
-		 * completes before it returns: ticket 0) */
-		if (pipe && s->ticket && rx_more(e))
-			e->cur ^= 1;   /* s stays in flight: the next call stages into p */
-		else
-			num_rx += rx_finish(e, s, out + num_rx, max_out - num_rx);
+	/* bursts are delivered in arrival order: a, then p, then s */
+	if (a->delivering)
+		num_rx += rx_dlv_end(e, a, out, max_out);
+	/* only a burst really in flight waits (a multi-GPU pktio's submit
+	 * completes before it returns: ticket 0) */
+	if (n > 0 && pipe && s->ticket && rx_more(e)) {
+		/* streaming: p's GPU delivery runs while the next call stages and
+		 * classifies, s stays in flight; the next call stages into a */
+		if (p->pending)
+			rx_finish_start(e, p);
+		e->cur = (e->cur + 1) % RX_SETS;
+		return num_rx;
 	}
+	if (p->pending)
+		num_rx += rx_finish(e, p, out + num_rx, max_out - num_rx);
+	if (n > 0)
+		num_rx += rx_finish(e, s, out + num_rx, max_out - num_rx);
 	return num_rx;
 }
 
@@ -1997,8 +2541,12 @@ int odp_amd_pktio_rx_idle(odp_pktio_t h)
 	if (!e)
 		return -1;
 	odp_spinlock_lock(&e->rxl);
-	if (e->rs[0].pending || e->rs[1].pending)
-		idle = 0;
+	idle = 1;
+	for (int k = 0; k < RX_SETS; k++)
+		if (e->rs[k].pending || e->rs[k].delivering)
+			idle = 0;
+	if (!idle)
+		;
 	else if (e->drv == DRV_PCAP)
 		idle = e->eof || e->nframes == 0 || (e->next >= e->nframes && e->loops == 1);
 	else if (e->drv == DRV_LOOP)

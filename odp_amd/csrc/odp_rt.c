@@ -504,6 +504,43 @@ static size_t align_up(size_t v, size_t a)
 	return (v + a - 1) / a * a;
 }
 
+static int pinned_pools(void)
+{
+	static int on = -1;
+
+	if (on < 0) {
+		const char *v = getenv("ODP_AMD_PINNED_POOLS");
+
+		on = !(v && v[0] == '0');
+	}
+	return on;
+}
+
+int rt_pinned_arena(uint8_t **lo, size_t *bytes)
+{
+	uint8_t *a = NULL, *b = NULL;
+
+	for (int i = 0; i < RT_MAX_POOLS; i++) {
+		const rt_pool_t *p = &RT.pool[i];
+
+		if (!p->used || !p->pinned || !p->mem)
+			continue;
+		if (!a || p->mem < a)
+			a = p->mem;
+		if (!b || p->mem + p->elem_size * p->num > b)
+			b = p->mem + p->elem_size * p->num;
+	}
+	*lo = a;
+	*bytes = a ? (size_t)(b - a) : 0;
+	return a != NULL;
+}
+
+uint32_t rt_data_from_meta(void)
+{
+	return (uint32_t)(align_up(sizeof(pkt_hdr_t), 64) + RT_PKT_HEADROOM -
+			  __builtin_offsetof(pkt_hdr_t, meta));
+}
+
 odp_pool_t odp_pool_create(const char *name, const odp_pool_param_t *param)
 {
 	size_t esz;
@@ -567,7 +604,19 @@ odp_pool_t odp_pool_create(const char *name, const odp_pool_param_t *param)
 
 	void *mem = NULL;
 
-	if (posix_memalign(&mem, 64, esz * num)) {
+	/* packet pools in page-locked memory the GPU addresses at the same
+	 * addresses: the receive path then classifies loop packets in place and
+	 * the GPU writes received packets' metadata and frames into them
+	 * (ODP_AMD_PINNED_POOLS=0: ordinary memory, host delivery) */
+	if (param->type == ODP_POOL_PACKET && pinned_pools()) {
+		mem = mi_cls_host_alloc(esz * num);
+		if (mem && !mi_cls_host_mapped(mem)) {
+			mi_cls_host_free(mem);
+			mem = NULL;
+		}
+		p->pinned = mem != NULL;
+	}
+	if (!mem && posix_memalign(&mem, 64, esz * num)) {
 		p->used = 0;
 		return ODP_POOL_INVALID;
 	}
@@ -578,7 +627,15 @@ odp_pool_t odp_pool_create(const char *name, const odp_pool_param_t *param)
 	p->param = *param;
 	snprintf(p->name, sizeof(p->name), "%s", name ? name : "");
 	odp_spinlock_init(&p->lock);
-	p->free_list = NULL;
+	p->free_stk = malloc((size_t)num * sizeof(ev_hdr_t *));
+	if (!p->free_stk) {
+		if (p->pinned)
+			mi_cls_host_free(p->mem);
+		else
+			free(p->mem);
+		p->used = 0;
+		return ODP_POOL_INVALID;
+	}
 	for (uint32_t i = num; i-- > 0;) {
 		ev_hdr_t *e = (ev_hdr_t *)(p->mem + (size_t)i * esz);
 
@@ -595,8 +652,8 @@ odp_pool_t odp_pool_create(const char *name, const odp_pool_param_t *param)
 		} else {
 			((evv_hdr_t *)e)->max_size = cap;
 		}
-		e->next = p->free_list;
-		p->free_list = e;
+		/* the stack's top is element 0 (taken first) */
+		p->free_stk[num - 1 - i] = e;
 	}
 	p->num_free = num;
 	return (odp_pool_t)(uintptr_t)(idx + 1);
@@ -611,7 +668,11 @@ int odp_pool_destroy(odp_pool_t h)
 	pool_cache_flush((int)(p - RT.pool));
 	if (p->num_free != p->num)
 		RT_ERR("pool %s destroyed with %u events in use\n", p->name, p->num - p->num_free);
-	free(p->mem);
+	if (p->pinned)
+		mi_cls_host_free(p->mem);
+	else
+		free(p->mem);
+	free(p->free_stk);
 	odp_spinlock_lock(&RT.lock);
 	memset(p, 0, sizeof(*p));
 	odp_spinlock_unlock(&RT.lock);
@@ -688,14 +749,11 @@ unsigned int odp_pool_max_index(void) { return RT_MAX_POOLS - 1; }
 
 static int pool_take(rt_pool_t *p, ev_hdr_t *out[], int num)
 {
-	int n = 0;
-
 	odp_spinlock_lock(&p->lock);
-	while (n < num && p->free_list) {
-		out[n++] = p->free_list;
-		p->free_list = p->free_list->next;
-	}
+	const int n = num < (int)p->num_free ? num : (int)p->num_free;
+
 	p->num_free -= (uint32_t)n;
+	memcpy(out, p->free_stk + p->num_free, (size_t)n * sizeof(ev_hdr_t *));
 	odp_spinlock_unlock(&p->lock);
 	return n;
 }
@@ -704,11 +762,8 @@ static void pool_give(rt_pool_t *p, ev_hdr_t *const e[], int num)
 {
 	if (num <= 0)
 		return;
-	for (int i = 0; i + 1 < num; i++)
-		e[i]->next = e[i + 1];
 	odp_spinlock_lock(&p->lock);
-	e[num - 1]->next = p->free_list;
-	p->free_list = e[0];
+	memcpy(p->free_stk + p->num_free, e, (size_t)num * sizeof(ev_hdr_t *));
 	p->num_free += (uint32_t)num;
 	odp_spinlock_unlock(&p->lock);
 }
@@ -1641,6 +1696,11 @@ int rt_queue_deq_multi_raw(rt_queue_t *q, odp_event_t ev[], int num)
 	odp_spinlock_lock(&q->lock);
 	r = ring_get(q, ev, num);
 	odp_spinlock_unlock(&q->lock);
+	/* the caller reads every event's first header line next (type, pool):
+	 * start all of those misses now (a packet's header was last written
+	 * by the GPU receive delivery or another core) */
+	for (int i = 0; i < r; i++)
+		__builtin_prefetch((const void *)ev[i]);
 	return r;
 }
 

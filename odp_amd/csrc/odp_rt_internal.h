@@ -9,6 +9,7 @@
 #include <pthread.h>
 
 #include "odp_api.h"
+#include "mi_cls.h"
 
 #define RT_MAX_POOLS   64
 #define RT_MAX_QUEUES  1024
@@ -33,23 +34,48 @@ typedef struct ev_hdr {
 } ev_hdr_t;
 
 /* packet metadata: the fields odp_packet_hdr_t carries on the receive path
- * (platform/linux-generic/include/odp_packet_internal.h:55-70,112-139) */
+ * (platform/linux-generic/include/odp_packet_internal.h:55-70,112-139).
+ * From data_off on they are mi_cls_pkt_meta_t, the block the GPU receive
+ * delivery writes (mi_cls_deliver_submit). */
 typedef struct pkt_hdr {
 	ev_hdr_t ev;
 	uint8_t *head;          /* buffer start */
 	uint32_t buf_len;       /* headroom + data capacity + tailroom */
-	uint32_t data_off;      /* current headroom */
-	uint32_t len;
 	uint32_t rsv;
-	uint64_t in_flags;      /* packet_parser_t.input_flags */
-	uint8_t err;            /* flags.all.error (7 bits) */
-	uint8_t cos;            /* CoS index, 0xff none */
-	uint16_t cls_mark;
-	uint16_t l2, l3, l4;
-	odp_queue_t dst_queue;
-	odp_pktio_t input;
-	const void *user_ptr;
+	/* the metadata block fills the header's second cache line: the GPU
+	 * writes it whole, and the line the pool and queues use stays the
+	 * host's */
+	uint8_t pad[32];
+	union {
+		mi_cls_pkt_meta_t meta;
+		struct {
+			uint32_t data_off;      /* current headroom */
+			uint32_t len;
+			uint64_t in_flags;      /* packet_parser_t.input_flags */
+			uint8_t err;            /* flags.all.error (7 bits) */
+			uint8_t cos;            /* CoS index, 0xff none */
+			uint16_t cls_mark;
+			uint16_t l2, l3, l4;
+			uint16_t rsv0;
+			uint32_t rsv1;
+			odp_queue_t dst_queue;
+			odp_pktio_t input;
+			const void *user_ptr;
+			uint64_t rsv2;
+		};
+	};
 } pkt_hdr_t;
+
+_Static_assert(sizeof(((pkt_hdr_t *)0)->meta) == 64 && __builtin_offsetof(pkt_hdr_t, meta) == 64 &&
+	       __builtin_offsetof(pkt_hdr_t, user_ptr) - __builtin_offsetof(pkt_hdr_t, meta) ==
+	       __builtin_offsetof(mi_cls_pkt_meta_t, user_ptr) &&
+	       __builtin_offsetof(pkt_hdr_t, dst_queue) - __builtin_offsetof(pkt_hdr_t, meta) ==
+	       __builtin_offsetof(mi_cls_pkt_meta_t, dst_queue) &&
+	       __builtin_offsetof(pkt_hdr_t, l4) - __builtin_offsetof(pkt_hdr_t, meta) ==
+	       __builtin_offsetof(mi_cls_pkt_meta_t, l4) &&
+	       __builtin_offsetof(pkt_hdr_t, in_flags) - __builtin_offsetof(pkt_hdr_t, meta) ==
+	       __builtin_offsetof(mi_cls_pkt_meta_t, in_flags),
+	       "pkt_hdr_t fields must overlay mi_cls_pkt_meta_t");
 
 typedef struct evv_hdr {
 	ev_hdr_t ev;
@@ -66,9 +92,12 @@ typedef struct rt_pool {
 	size_t elem_size;
 	uint32_t num;
 	uint32_t data_cap;      /* packet data capacity (excl. head/tailroom) */
-	ev_hdr_t *free_list;
-	uint32_t num_free;      /* on free_list (thread caches not counted) */
+	ev_hdr_t **free_stk;    /* free events: a stack of pointers (bulk take / give
+				 * copy pointers; no walk through the events) */
+	uint32_t num_free;      /* on free_stk (thread caches not counted) */
 	uint32_t gen;           /* creation number: tags the thread caches */
+	int pinned;             /* mem is page-locked and device-addressed at its host
+				 * addresses (GPU receive delivery reads / writes it) */
 	odp_spinlock_t lock;
 } rt_pool_t;
 
@@ -115,5 +144,11 @@ int rt_pktio_sched_poll(void);
 int rt_pktio_poll_index(int idx);
 uint32_t rt_gpu_index(void);
 int rt_queue_is_valid(odp_queue_t h);
+/* the address range spanned by the pinned packet pools ([*lo, *lo + *bytes));
+ * 0 when there is none */
+int rt_pinned_arena(uint8_t **lo, size_t *bytes);
+/* bytes from a packet header's metadata block to its data at the default
+ * headroom (fixed by the pool layout) */
+uint32_t rt_data_from_meta(void);
 
 #endif /* ODP_AMD_RT_INTERNAL_H_ */

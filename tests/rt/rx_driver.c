@@ -80,7 +80,8 @@ static odp_pool_t mkpool(const char *name)
 	 * runtime still keeps every packet in one segment, seg_len being the
 	 * minimum the spec asks for) */
 	p.pkt.seg_len = getenv("RX_SEG_LEN") ? (uint32_t)atoi(getenv("RX_SEG_LEN")) : 1856;
-	p.pkt.num = 20000;
+	/* RX_POOL_NUM: packets per pool (rate runs hold a whole capture) */
+	p.pkt.num = getenv("RX_POOL_NUM") ? (uint32_t)atoi(getenv("RX_POOL_NUM")) : 20000;
 	return odp_pool_create(name, &p);
 }
 
@@ -264,6 +265,42 @@ static void print_pkt(const char *q, odp_packet_t pkt)
 	printf("\n");
 }
 
+/* Send the source capture's frames into the loop interface through a
+ * parse-less pcap pktio (the loop "wire"); returns the frames sent. */
+static long feed_loop(const char *src_pcap, odp_pool_t pool, odp_pktio_t pktio)
+{
+	char src[512];
+	odp_pktio_param_t sp;
+	odp_pktio_config_t sc;
+	odp_pktin_queue_t inq;
+	odp_pktout_queue_t outq;
+	odp_packet_t pk[256];
+	int n;
+	long sent = 0;
+
+	snprintf(src, sizeof(src), "pcap:in=%s", src_pcap);
+	odp_pktio_param_init(&sp);
+	odp_pktio_t sio = odp_pktio_open(src, pool, &sp);
+
+	if (sio == ODP_PKTIO_INVALID || odp_pktin_queue_config(sio, NULL))
+		return -1;
+	odp_pktio_promisc_mode_set(sio, 1);
+	odp_pktio_config_init(&sc);
+	sc.parser.layer = ODP_PROTO_LAYER_NONE;
+	odp_pktio_config(sio, &sc);
+	if (odp_pktio_start(sio) || odp_pktin_queue(sio, &inq, 1) != 1 ||
+	    odp_pktout_queue(pktio, &outq, 1) < 1)
+		return -1;
+	while ((n = odp_pktin_recv(inq, pk, 256)) > 0) {
+		if (odp_pktout_send(outq, pk, n) != n)
+			return -1;
+		sent += n;
+	}
+	odp_pktio_stop(sio);
+	odp_pktio_close(sio);
+	return sent;
+}
+
 int main(int argc, char *argv[])
 {
 	odp_instance_t inst;
@@ -359,35 +396,18 @@ int main(int argc, char *argv[])
 	 * warm-up launch happen in odp_pktio_start */
 	odp_time_t t_start = odp_time_local();
 
-	/* loop: feed the source frames through a parse-less pcap pktio */
-	if (strncmp(argv[1], "loop", 4) == 0 && argc > 7) {
-		char src[512];
-		odp_pktio_param_t sp;
-		odp_pktio_config_t sc;
-		odp_pktin_queue_t inq;
-		odp_pktout_queue_t outq;
-		odp_packet_t pk[256];
-		int n;
+	/* loop: feed the source frames through a parse-less pcap pktio.
+	 * RX_LOOP_ROUNDS=R (rate runs, direct mode): R rounds of "send the
+	 * capture into the loop (not timed), receive and drain it (timed)" */
+	const int is_loop = strncmp(argv[1], "loop", 4) == 0 && argc > 7;
+	int rounds = getenv("RX_LOOP_ROUNDS") ? atoi(getenv("RX_LOOP_ROUNDS")) : 1;
+	uint64_t timed_ns = 0;
 
-		snprintf(src, sizeof(src), "pcap:in=%s", argv[7]);
-		odp_pktio_param_init(&sp);
-		odp_pktio_t sio = odp_pktio_open(src, pool, &sp);
-
-		if (sio == ODP_PKTIO_INVALID || odp_pktin_queue_config(sio, NULL))
-			return 9;
-		odp_pktio_promisc_mode_set(sio, 1);
-		odp_pktio_config_init(&sc);
-		sc.parser.layer = ODP_PROTO_LAYER_NONE;
-		odp_pktio_config(sio, &sc);
-		if (odp_pktio_start(sio) || odp_pktin_queue(sio, &inq, 1) != 1 ||
-		    odp_pktout_queue(pktio, &outq, 1) < 1)
-			return 9;
-		while ((n = odp_pktin_recv(inq, pk, 256)) > 0)
-			if (odp_pktout_send(outq, pk, n) != n)
-				return 10;
-		odp_pktio_stop(sio);
-		odp_pktio_close(sio);
-	}
+	if (is_loop && feed_loop(argv[7], pool, pktio) < 0)
+		return 9;
+	if (is_loop && rounds > 1)
+		t_start = odp_time_local();
+again:
 
 	if (pp.in_mode == ODP_PKTIN_MODE_DIRECT) {
 		odp_pktin_queue_t inq;
@@ -437,6 +457,13 @@ int main(int argc, char *argv[])
 			for (int i = 0; i < n; i++)
 				print_ev(qname(from), ev[i]);
 		}
+		if (is_loop && --rounds > 0) {
+			timed_ns += odp_time_diff_ns(odp_time_local(), t_start);
+			if (feed_loop(argv[7], pool, pktio) < 0)
+				return 9;
+			t_start = odp_time_local();
+			goto again;
+		}
 	} else {
 		int idle = 0;
 		odp_queue_t pin = ODP_QUEUE_INVALID;
@@ -464,7 +491,7 @@ int main(int argc, char *argv[])
 	}
 	if (count_only)
 		printf("R %" PRIu64 " %" PRIu64 "\n", delivered,
-		       odp_time_diff_ns(odp_time_local(), t_start));
+		       timed_ns + odp_time_diff_ns(odp_time_local(), t_start));
 	odp_pktio_stats_t st;
 
 	odp_pktio_stats(pktio, &st);

@@ -132,3 +132,83 @@ def test_group_host_batch_timing(built, gpu, ngroup):
     assert_same(got, exp, b, f"{ngroup} contexts")
     print(f"group classify_host: {ngroup} context(s), {b.n} packets, {dt * 1e3:.2f} ms per call, "
           f"{b.n / dt / 1e6:.1f} Mpkt/s")
+
+
+def _rx_rate(pc, rules, env):
+    """rx_driver rate mode (pcap pktio, direct): (Mpkt/s, delivered, in_discards)."""
+    import subprocess
+    e = dict(os.environ, RX_COUNT_ONLY="1", **env)
+    r = subprocess.run([H.DRIVER, f"pcap:in={pc}:loops=5", rules, "direct", "4", "0", "1"],
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=240,
+                       env=e)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rl = [ln for ln in r.stdout.splitlines() if ln.startswith("R ")][-1].split()
+    sl = [ln for ln in r.stdout.splitlines() if ln.startswith("S ")][-1].split()
+    return int(rl[1]) / int(rl[2]) * 1e3, int(rl[1]), int(sl[3])
+
+
+def test_runtime_pktio_group_pipelined_rate(built, gpu, tmp_path):
+    """A pcap pktio over 1 and 3 contexts (ODP_AMD_GPUS=0 / 0,0,0): with the
+    page-locked frame store each burst's slices are submitted to every
+    context and waited for one burst later (mi_cls_group_classify_host_submit
+    / _wait), so the group pktio keeps two bursts in flight like the single
+    one.  Every frame is delivered (0 in_discards); prints both rates."""
+    b, prog = R.config3(100_000)
+    pc = str(tmp_path / "in.pcap")
+    H.write_pcap(pc, [b.frame(i) for i in range(b.n)])
+    rules = str(tmp_path / "rules.txt")
+    H.write_rules(rules, prog)
+    res = {}
+    for gpus in ("0", "0,0,0"):
+        res[gpus] = _rx_rate(pc, rules, {"ODP_AMD_GPUS": gpus})
+        # loops=5 replays the capture as the reference's pcap driver does
+        # (pcap.c:257-278: the count starts at 1)
+        assert res[gpus][1] == res["0"][1] >= 4 * b.n and res[gpus][2] == 0, res
+    print("group pktio receive: " + ", ".join(f"{g}: {v[0]:.1f} Mpkt/s" for g, v in res.items()))
+
+
+def test_group_submit_tickets(built, gpu):
+    """odp_amd_cls_classify_host_submit / _wait on a 3-context pktio with
+    page-locked batches: three batches in flight at once, waited in order,
+    every record equal to the oracle's."""
+    import ctypes as C
+    import numpy as np
+    from odp_amd import cls
+    from odp_amd.cls import Classifier
+    L = cls.lib()
+    L.odp_amd_cls_classify_host_submit.restype = C.c_int
+    L.odp_amd_cls_classify_host_submit.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p,
+                                                   C.c_void_p, C.c_uint32, C.c_void_p,
+                                                   C.POINTER(C.c_uint64)]
+    L.odp_amd_cls_classify_host_wait.restype = C.c_int
+    L.odp_amd_cls_classify_host_wait.argtypes = [C.c_void_p, C.c_uint64]
+    batches = [R.config3(30_000 + 7 * k, rank=k)[0] for k in range(3)]
+    _, prog = R.config3(10)
+    c = Classifier(gpus=[0, 0, 0])
+    keep = []
+    try:
+        c.apply(prog)
+        tickets = []
+        for bt in batches:
+            pb = cls.PinnedArray(bt.buf.nbytes + 64)
+            po = cls.PinnedArray(4 * bt.n)
+            pl = cls.PinnedArray(2 * bt.n)
+            pr = cls.PinnedArray(16 * bt.n)
+            pb.u8[: bt.buf.nbytes] = bt.buf
+            po.view(np.uint32)[:] = bt.off
+            pl.view(np.uint16)[:] = bt.len
+            keep.append((pb, po, pl, pr))
+            t = C.c_uint64()
+            assert L.odp_amd_cls_classify_host_submit(c.pktio, pb.ptr, bt.buf.nbytes + 64, po.ptr,
+                                                      pl.ptr, bt.n, pr.ptr, C.byref(t)) == 0
+            tickets.append(t.value)
+        assert tickets == sorted(tickets) and tickets[0] > 0, tickets
+        for bt, t, (_, _, _, pr) in zip(batches, tickets, keep):
+            assert L.odp_amd_cls_classify_host_wait(c.pktio, t) == 0
+            got = pr.view(np.uint8, 16 * bt.n).view(R.RESULT_DTYPE).copy()
+            assert_same(got, oracle_run(prog, bt)[0], bt, f"ticket {t}")
+    finally:
+        c.close()
+        for arrs in keep:
+            for a in arrs:
+                a.close()

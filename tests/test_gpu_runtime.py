@@ -25,12 +25,13 @@ UDP64 = os.path.join(H.ROOT, "tests", "golden", "udp64.pcap")
 
 
 def _run_case(tmp_path, prog, frames, mode="sched", pktio="pcap", cos_pools=1, layer=4, cls=1,
-              burst=None, pktin_opt=0):
+              burst=None, pktin_opt=0, env_extra=None):
     pc = str(tmp_path / "in.pcap")
     H.write_pcap(pc, frames)
     rules = str(tmp_path / "rules.txt")
     H.write_rules(rules, prog)
     env = {"ODP_AMD_RX_BURST": str(burst)} if burst else {}
+    env.update(env_extra or {})
     if pktin_opt:
         env["RX_PKTIN_OPT"] = str(pktin_opt)
     if pktio == "loop":
@@ -90,6 +91,24 @@ def test_rx_zoo_shared_pool(built, gpu, tmp_path):
 def test_rx_loop_pktio(built, gpu, tmp_path):
     frames = H.pcap_frames([f for _, f in zoo.all_frames()])
     _run_case(tmp_path, zoo.prog_everything(), frames, pktio="loop")
+
+
+@pytest.mark.parametrize("cos_pools", [0, 1])
+@pytest.mark.parametrize("delivery", ["gpu", "host", "pageable_pools"])
+def test_rx_delivery_paths(built, gpu, tmp_path, cos_pools, delivery):
+    """The receive delivery after classification on both paths: the GPU
+    delivery kernel (page-locked pools: metadata, frame copies and the
+    group-by-queue done by mi_cls_deliver_submit; loop packets classified in
+    place, copied only on a pool switch) and the host's
+    (ODP_AMD_RX_GPU_DELIVER=0, or pools in ordinary memory).  pcap and loop
+    pktios, shared pool (in place) and per-CoS pools (pool switch); every
+    queue's packets, metadata and counters as the reference's."""
+    env = {"gpu": {}, "host": {"ODP_AMD_RX_GPU_DELIVER": "0"},
+           "pageable_pools": {"ODP_AMD_PINNED_POOLS": "0"}}[delivery]
+    frames = H.pcap_frames([f for _, f in zoo.all_frames()])
+    for pktio in ("pcap", "loop"):
+        _run_case(tmp_path, zoo.prog_everything(), frames, mode="direct", pktio=pktio,
+                  cos_pools=cos_pools, burst=61, env_extra=env)
 
 
 def test_rx_deletes_and_drops(built, gpu, tmp_path):
