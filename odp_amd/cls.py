@@ -322,14 +322,14 @@ class Classifier:
     def program_info(self) -> dict:
         """Device encoding of the current rule snapshot (host only)."""
         blob = self.compile()
-        info = (C.c_uint32 * 11)()
-        rc = self.L.mi_cls_program_info(blob, len(blob), info, 11)
+        info = (C.c_uint32 * 13)()
+        rc = self.L.mi_cls_program_info(blob, len(blob), info, 13)
         if rc:
             raise RuntimeError(f"mi_cls_program_info: {rc}")
         return {"words": info[0], "hot_words": info[1], "blocks": info[2],
                 "direct": info[3], "candidate": info[4], "bitmap": info[5], "wide": info[6],
                 "tree": bool(info[7]), "cand1": info[8], "flat_engine": int(info[9]) - 1,
-                "chained": info[10]}
+                "chained": info[10], "joint_direct": info[11], "joint_bitmap": info[12]}
 
     def spec_wait(self) -> int:
         """Snapshot the rules and wait for their program-specialised kernel

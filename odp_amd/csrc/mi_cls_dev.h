@@ -1194,7 +1194,9 @@ enum { DH_MAGIC = 0, DH_NCOS, DH_DEFAULT, DH_ERROR, DH_DEFAULT_VALID, DH_USED, D
        DH_HOT_OFF, DH_PROG_OFF, DH_TOTAL, DH_HOT_WORDS,
        // furthest byte past L3 / L4 / the frame start any term (or the hash
        // queue tuple) of the program reads: the kernel's window predictor
-       DH_L3END, DH_L4END, DH_FREND, DH_WORDS = 16 };
+       DH_L3END, DH_L4END, DH_FREND,
+       // hot-region word of the joint groups' directory (0: none)
+       DH_JOINT, DH_WORDS = 16 };
 #define DEV_MAGIC 0x33564544u   // "DEV3"
 #define REC_WORDS 16u
 #define COS_WORDS 4u
@@ -1220,6 +1222,22 @@ enum { DH_MAGIC = 0, DH_NCOS, DH_DEFAULT, DH_ERROR, DH_DEFAULT_VALID, DH_USED, D
 // direct blocks: a slot value / miss word is the rule's result word
 // (dst | leaf << 8 | mark << 16) with this bit set; 0 / BV_EMPTY: no rule
 #define BV_RES_VALID 0x200u
+// joint tables (tree programs): direct blocks sharing a class record, and
+// bitmap blocks over the same class records, probe one table per class over
+// (key, CoS); header word 1 of a direct member block, word 13 of a bitmap
+// member's class record (and word 6 of the class's info in the group's
+// info) say how the CoS slot enters the key: in 8 bits of a one-word key no
+// rule can set (at bit BVJ_SHIFT's value), or appended as the last key word.
+// Group info (hc[DH_JOINT + group - 1] = its word): kind (0 direct, 2
+// bitmap), #classes, alive rows and result-array words per CoS slot
+// (bitmap), then 8 words per class: class record, #buckets, table, m1, m2,
+// miss values per CoS slot, BVJ flags
+#define BVJ_ONEWORD 0x10000u
+#define BVJ_APPEND 0x20000u
+#define BVJ_SHIFT 18u
+// CoS entry word C_BV: block offset (bits 0-23), joint group + 1 (bits
+// 24-30, tree programs), chain of blocks (bit 31, flat programs)
+#define C_BV_OFF 0xFFFFFFu
 
 // Classification block of a CoS ("BV" block for historical reasons), used
 // when its rules fall into at most BV_MAX_CLS key classes (a key class is one
@@ -1496,6 +1514,21 @@ __device__ __forceinline__ uint32_t bv_probe(T H, const uint32_t key[4], bool ac
 	return val;
 }
 
+// The key of a joint group's table (BVJ_*): the CoS slot in 8 free bits of
+// a one-word key, or appended as the last key word (selects: nk may differ
+// per lane).
+__device__ __forceinline__ void joint_key(uint32_t flags, uint32_t cos, uint32_t key[4], uint32_t &nk)
+{
+	if (flags & BVJ_ONEWORD) {
+		key[0] |= cos << ((flags >> BVJ_SHIFT) & 31u);
+	} else if (flags & BVJ_APPEND) {
+		key[1] = nk == 1u ? cos : key[1];
+		key[2] = nk == 2u ? cos : key[2];
+		key[3] = nk == 3u ? cos : key[3];
+		++nk;
+	}
+}
+
 // the class record's own table
 template <typename D, typename T>
 __device__ __forceinline__ uint32_t bv_lookup(const D &cr, T H, const uint32_t key[4], bool act)
@@ -1530,7 +1563,7 @@ __device__ __forceinline__ bool split_key(const D &blk, uint32_t ro, bool act, c
 // `act` (BV_NONE: none); rule numbers index the block's result words.
 template <int FM, bool CHAIN, typename D, typename T>
 __device__ __forceinline__ uint32_t bv_first(const D &blk, const DescV &hb, T H, bool act,
-					     const Pkt &k, const Parsed &p, const Fields &x)
+					     const Pkt &k, const Parsed &p, const Fields &x, uint32_t cos = 0u)
 {
 	// header word 0: mode | next block of a chain << 8 (CHAIN kernels only)
 	const uint32_t mode = FM >= 0 ? (uint32_t)FM : (CHAIN ? (hb(0) & 0xffu) : hb(0)), ncls = hb(1);
@@ -1542,9 +1575,14 @@ __device__ __forceinline__ uint32_t bv_first(const D &blk, const DescV &hb, T H,
 		for (uint32_t kc = 0; kc < BV_MAX_CLS; ++kc) {
 			if (kc < ncls) {
 				const auto cr = blk.vec(8u + BV_CLS_WORDS * kc);
-				uint32_t key[4];
+				uint32_t key[4], nk = cr(1);
 				const bool present = bv_key(cr, k, p, x, key);
-				const uint32_t val = bv_lookup(cr, H, key, act && present);
+				// a joint group's member (tree programs): the class's table
+				// is the group's, keyed on (key, CoS) (record word 13)
+				if constexpr (!CHAIN)
+					joint_key(cr(13), cos, key, nk);
+				const uint32_t val = bv_probe(H, key, act && present, nk, cr(9), cr(10), cr(11),
+							      cr(12));
 				acc &= val != 0u ? val : cr(2);
 			}
 		}
@@ -1774,7 +1812,7 @@ __device__ __forceinline__ uint32_t chain_first(T H, cword_t hc, bool act, const
 template <int FM = -1, bool CHAIN = false, typename D, typename T>
 __device__ __forceinline__ void bv_eval(const D &blk, T H, bool act, const Pkt &k, const Parsed &p,
 					const Fields &x, uint32_t &hit, uint32_t &nxt, uint32_t &nmark,
-					uint32_t &nleaf)
+					uint32_t &nleaf, uint32_t cos = 0u)
 {
 	const auto hb = blk.hdr();   // the block header (words 0-7)
 	const uint32_t mode = FM >= 0 ? (uint32_t)FM : (CHAIN ? (hb(0) & 0xffu) : hb(0)), res = hb(2);
@@ -1786,6 +1824,8 @@ __device__ __forceinline__ void bv_eval(const D &blk, T H, bool act, const Pkt &
 		// holds the miss word and the table (bucket count, offset, m1, m2)
 		uint32_t key[4], nk;
 		const bool present = split_key(blk, hb(2), act, k, p, x, key, nk);
+		// a joint group's member: its table is the group's, keyed on (key, CoS)
+		joint_key(hb(1), cos, key, nk);
 		const uint32_t val = bv_probe(H, key, act && present, nk, hb(4), hb(5), hb(6), hb(7));
 		const uint32_t rw = val != 0u ? (val == BV_EMPTY ? 0u : val) : hb(3);
 		const bool h = act && rw != 0u;
@@ -1814,7 +1854,7 @@ __device__ __forceinline__ void bv_eval(const D &blk, T H, bool act, const Pkt &
 			ch = cur.hdr();
 		}
 	} else {
-		first = bv_first<FM, CHAIN>(blk, hb, H, act, k, p, x);
+		first = bv_first<FM, CHAIN>(blk, hb, H, act, k, p, x, cos);
 	}
 	const bool h = act && first != BV_NONE;
 	const uint32_t rw2 = H[res + (h ? first : 0u)];
@@ -1927,6 +1967,9 @@ __device__ __forceinline__ bool load_window(__amdgpu_buffer_rsrc_t rs, uint32_t 
 	// phase B only when some frame is longer than 64 B and the window
 	// predictor wants bytes 64.. (want_hi); otherwise a tile with long frames
 	// stages 64 B per frame and reads the rare bytes past them from HBM
+	// (staging only bytes 64..79, one 16-B load per frame -- enough for a
+	// QinQ IPv6 frame's ports -- measured slower and fetched more on config 5:
+	// 48.0 -> 54.2 us, 4.2 -> 4.7 KiB per tile)
 	const bool any_long = __ballot(len > 64u) != 0ull;
 	const bool hi = any_long && want_hi;
 	win = (any_long && !hi) ? 64u : (uint32_t)WIN;
@@ -2103,7 +2146,8 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 	const cword_t dce = hc + COS_WORDS * (uint32_t)max(def_cos, 0);
 	const uint32_t d_nr = def_cos >= 0 ? dce[C_NR] : 0u;
 	// bit 31: a chain of blocks (never set in tree programs)
-	const uint32_t d_bv = DIV ? dce[C_BV] : dce[C_BV] & 0x7fffffffu, d_rec0 = dce[C_REC0];
+	const uint32_t d_bv = DIV ? dce[C_BV] & C_BV_OFF : dce[C_BV] & 0x7fffffffu, d_rec0 = dce[C_REC0];
+	const uint32_t j_off = DIV ? dev[DH_JOINT] : 0u;   // joint groups' directory
 	const bool stats_on = a.stats != nullptr;
 	typedef typename std::conditional<LT, lword_t, gword_t>::type hot_t;
 	hot_t H;
@@ -2367,16 +2411,25 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 			} else {
 				if (d_bv != 0u && d_nr != 0u)
 					bv_eval<-1, !DIV>(DescU{ hc + d_bv, hc }, H, g, k, p, x, hit, nxt, nmark,
-							  nleaf);
+							  nleaf, (uint32_t)def_cos);
 				else
 					linear_scan(prog, d_rec0, d_nr, g, k, p, x, hit, nxt, nmark);
 			}
 			advance(g ? 1u : 0u, hit, nxt, nmark, nleaf);
 		}
+#ifdef DIAG_MAXROUND
+		uint32_t diag_round = 1;
+#endif
 		for (; FM < 0;) {
 			const unsigned long long pm = __ballot(pend != 0u);
 			if (pm == 0ull)
 				break;
+#ifdef DIAG_MAXROUND
+			// diagnostic timing variant: the descent stops after DIAG_MAXROUND
+			// rounds (records are wrong; never a shipped build)
+			if (++diag_round > DIAG_MAXROUND)
+				break;
+#endif
 			uint32_t hit = 0, nleaf = 0, nxt = 0, nmark = 0, handled = 0;
 			bool act = pend != 0u;
 			if constexpr (DIV) {
@@ -2384,12 +2437,65 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 				if (__ballot(pend != 0u && cur != c0) != 0ull) {
 					const uint32_t ci = COS_WORDS * (uint32_t)(pend != 0u ? cur : c0);
 					const uint32_t my_nr = H[ci + C_NR];
-					const uint32_t my_bv = H[ci + C_BV];
+					const uint32_t my_bw = H[ci + C_BV];
+					const uint32_t my_bv = my_bw & C_BV_OFF;
 					const bool empty = pend != 0u && my_nr == 0u;
 					const bool bvl = pend != 0u && my_nr != 0u && my_bv != 0u;
-					if (__ballot(bvl))
+					const unsigned long long bm = __ballot(bvl);
+					// every lane with a block sits on a CoS of one joint group:
+					// the group's words in SGPRs, one probe per lane and class of
+					// the group's (key, CoS) tables, no per-lane block reads
+					const uint32_t jg = (my_bw >> 24) & 0x7fu;
+					const uint32_t g0 = bm ? (uint32_t)__builtin_amdgcn_readlane(
+									 (int)jg, (int)__builtin_ctzll(bm)) : 0u;
+					if (g0 != 0u && __ballot(bvl && jg != g0) == 0ull) {
+						const DescU jd{ hc + hc[j_off + g0 - 1u], hc };
+						const auto ji = jd.vec(0u);
+						const uint32_t cs = bvl ? (uint32_t)cur : 0u;
+						uint32_t rw;
+						bool hv;
+						if (ji(0) == 0u) {
+							// direct: the first live rule's result word
+							const auto cr = DescU{ hc + ji(8), hc }.vec(0u);
+							uint32_t key[4], nk = cr(1);
+							const bool present = bv_key(cr, k, p, x, key);
+							joint_key(ji(14), cs, key, nk);
+							const uint32_t val = bv_probe(H, key, bvl && present, nk, ji(9),
+										      ji(10), ji(11), ji(12));
+							const uint32_t miss = H[ji(13) + cs];
+							rw = val != 0u ? (val == BV_EMPTY ? 0u : val) : miss;
+							hv = rw != 0u;
+						} else {
+							// bitmap: AND of the classes' rule rows and the
+							// CoS's alive row, then its result word
+							const uint32_t ncls = ji(1);
+							uint32_t acc = H[ji(2) + cs];
+#pragma unroll
+							for (uint32_t kc = 0; kc < BV_MAX_CLS; ++kc) {
+								if (kc < ncls) {
+									const auto ci = jd.vec(8u + 8u * kc);
+									const auto cr = DescU{ hc + ci(0), hc }.vec(0u);
+									uint32_t key[4], nk = cr(1);
+									const bool present = bv_key(cr, k, p, x, key);
+									joint_key(ci(6), cs, key, nk);
+									const uint32_t val = bv_probe(H, key, bvl && present, nk,
+												      ci(1), ci(2), ci(3), ci(4));
+									acc &= val != 0u ? val : H[ci(5) + cs];
+								}
+							}
+							const uint32_t res = H[ji(3) + cs];
+							rw = H[res + (acc != 0u ? (uint32_t)__builtin_ctz(acc) : 0u)];
+							hv = acc != 0u;
+						}
+						const bool h = bvl && hv;
+						nxt = h ? (rw & 0xffu) : nxt;
+						nleaf = h ? ((rw >> 8) & 1u) : nleaf;
+						nmark = h ? (rw >> 16) : nmark;
+						hit = h ? 1u : hit;
+					} else if (bm) {
 						bv_eval(DescL<hot_t>{ H, my_bv, hc }, H, bvl, k, p, x, hit, nxt, nmark,
-							nleaf);
+							nleaf, (uint32_t)cur);
+					}
 					handled = (bvl || empty) ? 1u : 0u;
 					act = pend != 0u && handled == 0u;
 				}
@@ -2401,10 +2507,10 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 				const bool g = act && cur == c1;
 				grp = g ? 1u : 0u;
 				const cword_t ce = hc + COS_WORDS * (uint32_t)c1;
-				const uint32_t nr = ce[C_NR], bv = DIV ? ce[C_BV] : ce[C_BV] & 0x7fffffffu;
+				const uint32_t nr = ce[C_NR], bv = DIV ? ce[C_BV] & C_BV_OFF : ce[C_BV] & 0x7fffffffu;
 				if (bv != 0u && nr != 0u)
 					bv_eval<-1, !DIV>(DescU{ hc + bv, hc }, H, g, k, p, x, hit, nxt, nmark,
-							  nleaf);
+							  nleaf, (uint32_t)c1);
 				else
 					linear_scan(prog, ce[C_REC0], nr, g, k, p, x, hit, nxt, nmark);
 			}

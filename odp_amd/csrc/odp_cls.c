@@ -1254,6 +1254,23 @@ int odp_amd_cls_cos_enq_mode(uint32_t cos_index, odp_pool_t *vec_pool, uint32_t 
 	return c->use_std_enq;
 }
 
+/* 1 when every valid CoS has a pool of its own: classified packets never
+ * come from the pktio's pool (the receive path's pcap burst bound). */
+int odp_amd_cls_all_cos_pooled(void)
+{
+	int all = 1, any = 0;
+
+	pthread_mutex_lock(&G.lock);
+	for (uint32_t i = 0; G.init && i < G.max_cos; i++)
+		if (G.cos[i].valid) {
+			any = 1;
+			if (G.cos[i].pool == ODP_POOL_INVALID)
+				all = 0;
+		}
+	pthread_mutex_unlock(&G.lock);
+	return any && all;
+}
+
 /* cos->pool of the final CoS (_odp_cls_classify_packet, :1760-1764) */
 odp_pool_t odp_amd_cls_pool_of(uint32_t cos_index)
 {

@@ -2264,7 +2264,9 @@ static int pktio_recv(rt_pktio_t *e, odp_packet_t out[], int max_out)
 		 * so a packet allocation never fails on a staged frame (frames not
 		 * staged stay in the store for the next call; the reference instead
 		 * consumes the frame and stops on a failed allocation, pcap.c:324-327) */
-		if (rt_pool(e->pool)) {
+		/* (frames that all go to CoS with pools of their own never take a
+		 * packet of the pktio's pool: no bound then) */
+		if (rt_pool(e->pool) && !(e->cls_enabled && odp_amd_cls_all_cos_pooled())) {
 			long room = (long)rt_pool_avail(e->pool) - (p->pending ? (long)p->n : 0);
 
 			if (room < (long)burst)

@@ -324,6 +324,18 @@ int main(int argc, char *argv[])
 		return 3;
 	odp_schedule_config(NULL);
 	odp_pool_t pool = mkpool("pktio_pool");
+	/* RX_HOLD_PKTIO_POOL=1: every packet of the pktio's pool is held by the
+	 * application for the run (classified frames then need CoS pools) */
+	odp_packet_t *held = NULL;
+	int nheld = 0;
+
+	if (getenv("RX_HOLD_PKTIO_POOL")) {
+		held = malloc(sizeof(odp_packet_t) * 1048576);
+		odp_packet_t pk;
+
+		while (held && nheld < 1048576 && (pk = odp_packet_alloc(pool, 64)) != ODP_PACKET_INVALID)
+			held[nheld++] = pk;
+	}
 
 	if (getenv("RX_PKTV")) {
 		odp_pool_param_t vp;
@@ -512,6 +524,10 @@ again:
 	fprintf(stderr, "T loop done %.1f ms\n", odp_time_diff_ns(odp_time_local(), t_start) / 1e6);
 	odp_pktio_stop(pktio);
 	fprintf(stderr, "T stopped %.1f ms\n", odp_time_diff_ns(odp_time_local(), t_start) / 1e6);
+	if (held) {
+		odp_packet_free_multi(held, nheld);
+		free(held);
+	}
 	odp_pktio_close(pktio);
 	fprintf(stderr, "T closed %.1f ms\n", odp_time_diff_ns(odp_time_local(), t_start) / 1e6);
 	return 0;

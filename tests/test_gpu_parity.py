@@ -29,6 +29,7 @@ ENGINE_ENV = {
     "noflat": {"MI_CLS_NO_FLAT": "1"},   # general kernel for flat programs too
     "spec": {},                          # program-specialised kernel (waited for)
     "nojit": {"MI_CLS_JIT": "0"},        # no specialised kernels
+    "nojoint": {"MI_CLS_NO_JOINT": "1"},   # no joint direct tables for tree levels
 }
 
 
@@ -38,7 +39,7 @@ def both(prog, batch, limits=(255, 8192, 4096), what="", engine="auto"):
     force one of the kernel's paths (ENGINE_ENV)."""
     import os
     keys = ("MI_CLS_NO_BV", "MI_CLS_DIV", "MI_CLS_WPB", "MI_CLS_NO_WIDE", "MI_CLS_NO_CAND1",
-            "MI_CLS_NO_PORTMERGE", "MI_CLS_NO_FLAT", "MI_CLS_JIT")
+            "MI_CLS_NO_PORTMERGE", "MI_CLS_NO_FLAT", "MI_CLS_JIT", "MI_CLS_NO_JOINT")
     old = {k: os.environ.pop(k, None) for k in keys}
     os.environ.update(ENGINE_ENV[engine])
     try:
@@ -102,7 +103,7 @@ def test_zoo_no_default(built, gpu):
 
 
 @pytest.mark.parametrize("engine", ["auto", "linear", "nodiv", "div", "wpb16", "nowide", "nocand1",
-                                    "noportmerge", "noflat", "spec", "nojit"])
+                                    "noportmerge", "noflat", "spec", "nojit", "nojoint"])
 @pytest.mark.parametrize("seed", range(12))
 def test_random_programs_fuzz(built, gpu, seed, engine):
     rng = np.random.default_rng(1000 + seed)
@@ -116,7 +117,7 @@ def test_random_programs_fuzz(built, gpu, seed, engine):
 
 
 @pytest.mark.parametrize("engine", ["auto", "linear", "nodiv", "wpb4", "wpb16", "nowide", "nocand1",
-                                    "noportmerge", "noflat", "spec", "nojit"])
+                                    "noportmerge", "noflat", "spec", "nojit", "nojoint"])
 @pytest.mark.parametrize("cfg,n", [(1, 10_000), (2, 100_000), (3, 50_000), (4, 50_000),
                                    (5, 20_000)])
 def test_configs_small(built, gpu, cfg, n, engine):
@@ -132,6 +133,69 @@ def test_wide_rule_counts(built, gpu, num_rules, engine):
     rules on one CoS) and just past it (257: candidate lists)."""
     b, prog = R.config3(20_000, num_rules=num_rules, size=60)
     both(prog, b, what=f"{num_rules} rules", engine=engine)
+
+
+def _joint_tree(rng, n, leaf_kind):
+    """Default CoS -> 6 VLAN_ID_0 rules -> 6 mid CoS; each mid CoS's rules
+    share one class (so the mid level is a joint direct group): 12 rules of
+    leaf_kind each to 24 leaf CoS (marks); half the traffic hits."""
+    prog = [R.cos("default", queue=1)]
+    mids = list(range(1, 7))
+    prog += [R.cos(f"mid{i}", queue=10 + i) for i in range(6)]
+    leaves = list(range(7, 31))
+    prog += [R.cos(f"leaf{i}", queue=50 + i, action=1 if i == 23 else 0) for i in range(24)]
+    prog.append(("default", 0))
+    vids = [200 + 3 * i for i in range(6)]
+    for i in range(6):
+        prog.append(("pmr", [R.t_be16(R.PMR_VLAN_ID_0, vids[i], 0x0FFF)], 0, mids[i], 0))
+    vals = {}
+    for i in range(6):
+        for j in range(12):
+            if leaf_kind == "dport":
+                v = 5000 + 11 * j + i
+                t = R.t_be16(R.PMR_UDP_DPORT if j % 3 else R.PMR_TCP_DPORT, v)
+            elif leaf_kind == "dip":
+                v = (10 << 24) | (i << 16) | (j << 8) | 7
+                t = R.t_ip4(R.PMR_DIP_ADDR, v.to_bytes(4, "big"), 32)
+            else:   # sip6 /64
+                v = bytes([0x20, 0x01, 0x0d, 0xb8, 0, i, 0, j]) + bytes(8)
+                t = R.t_ip6(R.PMR_SIP6_ADDR, v, 64)
+            vals[(i, j)] = v
+            prog.append(("pmr", [t], mids[i], leaves[(i * 12 + j) % 24], (i * 16 + j) & 0xFFFF))
+    hit = rng.random(n) < 0.5
+    i = rng.integers(0, 6, n)
+    j = rng.integers(0, 12, n)
+    ipver = np.full(n, 6 if leaf_kind == "sip6" else 4)
+    proto = np.where(j % 3 == 0, pg.IPPROTO_TCP, pg.IPPROTO_UDP)
+    dport = np.where(hit & (leaf_kind == "dport"), 5000 + 11 * j + i, rng.integers(1, 65535, n))
+    dip4 = np.where(hit & (leaf_kind == "dip"), (10 << 24) | (i << 16) | (j << 8) | 7,
+                    rng.integers(0, 2 ** 32, n)).astype(np.uint64)
+    sip6 = rng.integers(0, 256, (n, 16)).astype(np.uint8)
+    if leaf_kind == "sip6":
+        for k in np.nonzero(hit)[0]:
+            sip6[k, :8] = np.frombuffer(vals[(int(i[k]), int(j[k]))][:8], np.uint8)
+    vid0 = np.where(rng.random(n) < 0.9, np.array(vids)[i], 999)
+    b = pg.build_batch(np.where(rng.random(n) < 0.7, 60, 300), ipver=ipver, l4proto=proto,
+                       sip4=rng.integers(0, 2 ** 32, n).astype(np.uint64), dip4=dip4, sip6=sip6,
+                       dip6=rng.integers(0, 256, (n, 16)).astype(np.uint8),
+                       sport=rng.integers(1, 65535, n), dport=dport,
+                       ntags=np.where(rng.random(n) < 0.2, 2, 1), vid0=vid0,
+                       vid1=rng.integers(1, 4095, n), seed=7)
+    return b, prog
+
+
+@pytest.mark.parametrize("engine", ["auto", "nojoint", "wpb4", "linear"])
+@pytest.mark.parametrize("leaf_kind", ["dport", "dip", "sip6"])
+def test_joint_direct_tree_levels(built, gpu, leaf_kind, engine):
+    """A tree level whose CoS all key on one class is one joint direct group
+    (one-word keys with the CoS slot in free bits for merged ports, the slot
+    appended for a /32 DIP and a two-word SIP6 /64 key): every record
+    bit-exact against the oracle, with and without joint tables."""
+    rng = np.random.default_rng({"dport": 1, "dip": 2, "sip6": 3}[leaf_kind])
+    b, prog = _joint_tree(rng, 30_000, leaf_kind)
+    got = both(prog, b, what=f"joint {leaf_kind}", engine=engine)
+    s = summary(got)
+    assert s["enq"] > 0 and s["cos_drop"] > 0
 
 
 def test_config2_tree_equals_flat(built, gpu):
@@ -306,6 +370,50 @@ def test_overlapping_acls(built, gpu, name, make, engine):
     b, prog = make(50_000)
     got = both(prog, b, what=name, engine=engine)
     assert summary(got)["enq"] > 0
+
+
+def _shadow_prog(variant):
+    """Rules that can never be the first holding rule beside rules that can
+    (ADVICE r3): exact duplicates with different destinations and marks, a
+    superset rule before and after its subset, and a rule without terms in
+    the middle of the list; first match in scan order decides."""
+    net = lambda a, p: R.t_ip4(R.PMR_SIP_ADDR, a, p)
+    port = lambda v: R.t_be16(R.PMR_UDP_DPORT, v)
+    prog = [R.cos("d", queue=1)] + [R.cos(f"c{i}", queue=10 + i) for i in range(8)]
+    prog.append(("default", 0))
+    rules = [
+        ([net("10.0.0.0", 24), port(53)], 1, 11),
+        ([net("10.0.0.0", 24), port(53)], 2, 12),          # exact duplicate: shadowed
+        ([net("10.0.0.0", 24), port(53), R.t_u8(R.PMR_IPPROTO, 17)], 3, 13),   # superset after
+        ([net("10.0.1.0", 24), port(80), R.t_u8(R.PMR_IPPROTO, 17)], 4, 14),   # superset before
+        ([net("10.0.1.0", 24), port(80)], 5, 15),          # its subset, later
+        ([net("10.0.2.0", 24)], 6, 16),
+        ([], 7, 17) if variant == "wildcard_mid" else ([net("10.0.3.0", 24)], 7, 17),
+        ([net("10.0.2.0", 24), port(443)], 8, 18),         # behind the /24 (shadowed)
+        ([net("10.0.4.0", 24), port(8080)], 1, 19),
+    ]
+    for terms, dst, mark in rules:
+        prog.append(("pmr", terms, 0, dst, mark))
+    return prog
+
+
+@pytest.mark.parametrize("engine", ["auto", "spec", "nocand1", "linear"])
+@pytest.mark.parametrize("variant", ["plain", "wildcard_mid"])
+def test_shadowed_rules_first_match(built, gpu, variant, engine):
+    """First-match parity where block build drops shadowed rules (ADVICE r3:
+    the engine-selection test alone did not pin which rule wins)."""
+    rng = np.random.default_rng(77)
+    n = 20_000
+    nets = np.array([(10 << 24) | (k << 8) | 5 for k in range(6)], dtype=np.uint64)
+    sip = nets[rng.integers(0, 6, n)]
+    dport = np.array([53, 80, 443, 8080, 9])[rng.integers(0, 5, n)]
+    proto = np.where(rng.random(n) < 0.8, pg.IPPROTO_UDP, pg.IPPROTO_TCP)
+    b = pg.build_batch(np.full(n, 60), ipver=np.full(n, 4), l4proto=proto, sip4=sip,
+                       dip4=rng.integers(0, 2 ** 32, n).astype(np.uint64), sport=np.full(n, 1000),
+                       dport=dport, seed=3)
+    got = both(_shadow_prog(variant), b, what=f"shadowed {variant}", engine=engine)
+    # the wildcard rule in the middle takes every packet no earlier rule holds
+    assert len(np.unique(got["cos"])) >= (4 if variant == "wildcard_mid" else 5)
 
 
 def _under_root(prog, root_first=False):

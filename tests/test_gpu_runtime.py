@@ -111,6 +111,17 @@ def test_rx_delivery_paths(built, gpu, tmp_path, cos_pools, delivery):
                   cos_pools=cos_pools, burst=61, env_extra=env)
 
 
+def test_rx_pktio_pool_held_cos_pools(built, gpu, tmp_path):
+    """Every packet of the pktio's pool held by the application while every
+    CoS has a pool of its own: the pcap receive keeps moving --
+    the frames never need the pktio's pool -- and delivers what the
+    reference delivers."""
+    frames = H.pcap_frames([f for _, f in zoo.all_frames()])
+    prog = [op for op in zoo.prog_everything()]
+    _run_case(tmp_path, prog, frames, mode="direct", cos_pools=1,
+              env_extra={"RX_HOLD_PKTIO_POOL": "1"})
+
+
 def test_rx_deletes_and_drops(built, gpu, tmp_path):
     frames = H.pcap_frames([f for _, f in zoo.all_frames()])
     _run_case(tmp_path, zoo.prog_deletes(), frames)

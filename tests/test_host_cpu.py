@@ -283,3 +283,27 @@ def test_shadowed_rules_leave_candidate_lists(built):
         assert info["cand1"] == 1 and info["candidate"] == 0, info
     finally:
         c.close()
+
+
+def test_joint_groups_host(built):
+    """Tree levels keyed on the same classes assemble into joint groups: one
+    (key, CoS) table per level and class instead of a table per CoS -- config
+    5's direct level (128 CoS) and its bitmap level (16 CoS);
+    MI_CLS_NO_JOINT=1: per-CoS tables.  Host only; GPU parity:
+    tests/test_gpu_parity.py test_joint_direct_tree_levels and the configs."""
+    def hot_words():
+        c = cls.Classifier(gpu=0)
+        try:
+            c.apply(R.config5(100)[1])
+            return c.program_info()
+        finally:
+            c.close()
+    with_joint = hot_words()
+    os.environ["MI_CLS_NO_JOINT"] = "1"
+    try:
+        without = hot_words()
+    finally:
+        del os.environ["MI_CLS_NO_JOINT"]
+    assert with_joint["tree"] and with_joint["direct"] == without["direct"]
+    assert with_joint["joint_direct"] == 128 and with_joint["joint_bitmap"] == 16, with_joint
+    assert without["joint_direct"] == 0 and without["joint_bitmap"] == 0, without
