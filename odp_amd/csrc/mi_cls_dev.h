@@ -532,10 +532,23 @@ __device__ __forceinline__ uint32_t ck_sum_wave(__amdgpu_buffer_rsrc_t rs, uint3
 		const int32_t lb = (int32_t)(pr & 63u) - (int32_t)(64u * q);
 		const int32_t hb = (int32_t)(pr >> 6) - (int32_t)(64u * q);
 		u32x4 v[4];
+#ifdef DIAG_CK_COALESCED
+		// diagnostic timing variant: load k of lane j reads part j & 3 of
+		// the round's piece 16 k + j / 4 (each load covers 16 whole pieces;
+		// the sums are wrong)
+#pragma unroll
+		for (uint32_t k = 0; k < 4; ++k) {
+			const uint32_t src = 16u * k + (lane >> 2);
+			const uint32_t o2 = lane_get(ob, src) + 16u * (lane & 3u);
+			v[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, lane_get(live ? 1u : 0u, src) ? o2 : OOB_OFF,
+								    0, 0);
+		}
+#else
 #pragma unroll
 		for (int32_t k = 0; k < 4; ++k)   // only 16-B parts that reach into [from, to)
 			v[k] = __builtin_amdgcn_raw_buffer_load_b128(
 				rs, (live && 16 * k < hb && 16 * k + 16 > lb) ? ob + 16u * k : OOB_OFF, 0, 0);
+#endif
 		const bool ph = live && lb > 0 && (lb & 3) != 0;
 		const bool pt = live && hb < 64 && (hb & 3) != 0;
 		const uint32_t xh = __builtin_amdgcn_raw_buffer_load_b32(
@@ -683,17 +696,38 @@ __device__ __forceinline__ uint32_t sctp_crc_wave(__amdgpu_buffer_rsrc_t rs, uin
 		const uint32_t ob = lane_get(p0, lo) + 64u * k;
 		const bool live = g < total;
 		u32x4 v[4];
+#ifdef DIAG_CK_COALESCED
+#pragma unroll
+		for (uint32_t i = 0; i < 4; ++i) {
+			const uint32_t src = 16u * i + (lane >> 2);
+			const uint32_t o2 = lane_get(ob, src) + 16u * (lane & 3u);
+			v[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, lane_get(live ? 1u : 0u, src) ? o2 : OOB_OFF,
+								    0, 0);
+		}
+#else
 #pragma unroll
 		for (uint32_t i = 0; i < 4; ++i)
 			v[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, live ? ob + 16u * i : OOB_OFF, 0, 0);
+#endif
 		uint32_t crc = 0;
+#ifdef DIAG_CRC_NOCHAIN
+		// diagnostic timing variant: the words XORed, no table steps
+#pragma unroll
+		for (uint32_t d = 0; d < 16; ++d)
+			crc ^= v[d >> 2][d & 3];
+#else
 #pragma unroll
 		for (uint32_t d = 0; d < 16; ++d) {
 			const uint32_t w = v[d >> 2][d & 3];
 			crc = crc32c_u32(tab, crc, (d == 2u && k == 0u) ? 0u : w);   // the checksum field
 		}
+#endif
 		// shift by the full pieces after this one
+#ifdef DIAG_CRC_NOMUL
+		const uint32_t r = live ? crc ^ zt[min(fnf - 1u - k, (uint32_t)CRC_ZN - 1u)] : 0u;
+#else
 		const uint32_t r = live ? crc_mulmod(crc, zt[min(fnf - 1u - k, (uint32_t)CRC_ZN - 1u)]) : 0u;
+#endif
 		const uint32_t P = wave_scan_xor(r, lane);
 		const uint32_t a0 = first > B ? first - B : 0u;
 		const uint32_t e = min(incl > B ? incl - B : 0u, (uint32_t)WAVE);
@@ -704,6 +738,7 @@ __device__ __forceinline__ uint32_t sctp_crc_wave(__amdgpu_buffer_rsrc_t rs, uin
 	// the full pieces sit rr bytes before the frame end
 	acc = (ask && nf) ? crc_mulmod(acc, yt[rr]) : 0u;
 	// the partial piece, walked by its owner: words, then 0-3 bytes
+#ifndef DIAG_CRC_NOTAIL
 	{
 		const uint32_t pb = p0 + 64u * nf;   // its first byte
 		u32x4 v[4];
@@ -736,6 +771,7 @@ __device__ __forceinline__ uint32_t sctp_crc_wave(__amdgpu_buffer_rsrc_t rs, uin
 		}
 		acc ^= crc;
 	}
+#endif
 	// the init register ~0 shifted over the whole message
 	const uint32_t sh = crc_mulmod(zt[min(n >> 6, (uint32_t)CRC_ZN - 1u)], yt[n & 63u]);
 	return ~(acc ^ crc_mulmod(0xFFFFFFFFu, sh));
