@@ -415,16 +415,38 @@ __device__ __forceinline__ Parsed parse_packet(const Pkt &k, uint32_t opt)
 // caller-supplied init, no final inversion), as slicing-by-4 tables: t[0] is
 // the byte table, t[k][i] = t[k-1][i] >> 8 ^ t[0][t[k-1][i] & 0xff], so four
 // bytes advance with four independent lookups instead of four dependent ones.
-// z[m] = x^(512 m) and y[r] = x^(8 r) mod P in the reflected domain (the
-// register that m 64-byte / r one-byte zero blocks turn 0x80000000 = x^0
-// into): the shifts that combine CRCs of separately processed pieces
-// (sctp_crc_wave; zlib's crc32_combine arithmetic).
+// s128 / s256: the register advanced over 16 / 32 zero bytes, per register
+// byte (s[k][b] = advance(b << 8k)), to join the raw CRCs of consecutive
+// 16-B / 32-B chunks with four lookups.  z[m] = x^(512 m), yinv[z] =
+// x^(-8 z) and y1[r] = ~0 x^(8 r) mod P in the reflected domain (x^0 =
+// 0x80000000): the shifts that combine CRCs of separately processed pieces
+// (sctp_crc_wave; zlib's crc32_combine arithmetic).  x^-1 exists (P has a
+// constant term): (P + 1) / x, i.e. (0x82F63B78 << 1) | 1.
 #define CRC_ZN 256          // pieces of 64 B a frame may have on the cooperative path
+// word offsets of the tables in the kernel's LDS copy
+#define CRC_S128 1024u
+#define CRC_S256 2048u
+#define CRC_Z 3072u
+#define CRC_YINV (CRC_Z + CRC_ZN)
+#define CRC_Y1 (CRC_YINV + 65u)
+#define CRC_WORDS (CRC_Y1 + 64u)
+__host__ __device__ constexpr uint32_t crc_mulmod_c(uint32_t a, uint32_t b)
+{
+	uint32_t p = 0;
+	for (int i = 31; i >= 0; --i) {
+		p ^= ((a >> i) & 1u) ? b : 0u;
+		b = (b >> 1) ^ ((b & 1u) ? 0x82F63B78u : 0u);
+	}
+	return p;
+}
 struct Crc32cTab {
 	uint32_t t[4][256];
+	uint32_t s128[4][256];
+	uint32_t s256[4][256];
 	uint32_t z[CRC_ZN];
-	uint32_t y[64];
-	constexpr Crc32cTab() : t(), z(), y()
+	uint32_t yinv[65];
+	uint32_t y1[64];
+	constexpr Crc32cTab() : t(), s128(), s256(), z(), yinv(), y1()
 	{
 		for (uint32_t i = 0; i < 256; ++i) {
 			uint32_t c = i;
@@ -435,17 +457,35 @@ struct Crc32cTab {
 		for (int k = 1; k < 4; ++k)
 			for (uint32_t i = 0; i < 256; ++i)
 				t[k][i] = (t[k - 1][i] >> 8) ^ t[0][t[k - 1][i] & 0xffu];
+		for (int k = 0; k < 4; ++k)
+			for (uint32_t i = 0; i < 256; ++i) {
+				uint32_t r = i << (8 * k);
+				for (int j = 0; j < 32; ++j) {
+					if (j == 16)
+						s128[k][i] = r;
+					r = t[0][r & 0xffu] ^ (r >> 8);
+				}
+				s256[k][i] = r;
+			}
 		uint32_t r = 0x80000000u;
-		for (uint32_t i = 0; i < 64; ++i) {
-			y[i] = r;
-			r = t[0][r & 0xffu] ^ (r >> 8);
-		}
-		r = 0x80000000u;
 		for (uint32_t m = 0; m < CRC_ZN; ++m) {
 			z[m] = r;
 			for (int i = 0; i < 16; ++i)   // 64 zero bytes, four at a time
 				r = t[3][r & 0xffu] ^ t[2][(r >> 8) & 0xffu] ^ t[1][(r >> 16) & 0xffu] ^
 				    t[0][r >> 24];
+		}
+		uint32_t xi8 = 0x80000000u;   // x^-8
+		for (int i = 0; i < 8; ++i)
+			xi8 = crc_mulmod_c(xi8, (0x82F63B78u << 1) | 1u);
+		r = 0x80000000u;
+		for (uint32_t i = 0; i < 65; ++i) {
+			yinv[i] = r;
+			r = crc_mulmod_c(r, xi8);
+		}
+		r = 0xFFFFFFFFu;
+		for (uint32_t i = 0; i < 64; ++i) {
+			y1[i] = r;
+			r = t[0][r & 0xffu] ^ (r >> 8);
 		}
 	}
 };
@@ -509,6 +549,9 @@ __device__ __forceinline__ uint32_t wave_scan_add(uint32_t v, uint32_t lane)
 // prefix sum over the round gives each owner its pieces' total as the
 // difference of two prefix values.  Returns the lane's own sum (congruent
 // mod 0xffff, < 2^32).
+#ifndef CK_HALVES
+#define CK_HALVES 1         // pieces per lane per round of ck_sum_wave (A/B: 2, 3 slower)
+#endif
 __device__ __forceinline__ uint32_t ck_sum_wave(__amdgpu_buffer_rsrc_t rs, uint32_t base,
 						uint32_t prm, uint32_t cnt, uint32_t lane)
 {
@@ -516,62 +559,84 @@ __device__ __forceinline__ uint32_t ck_sum_wave(__amdgpu_buffer_rsrc_t rs, uint3
 	const uint32_t first = incl - cnt;   // number of this lane's first piece
 	const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, WAVE - 1);
 	uint32_t acc = 0;
-	for (uint32_t B = 0; B < total; B += WAVE) {
-		const uint32_t g = B + lane;
-		uint32_t lo = 0;
+	// CK_HALVES pieces per lane per round (lane j takes pieces B + j and B +
+	// 64 + j): the loads of both are in flight together, so a round trip to
+	// memory serves twice the bytes (the sum phase is latency-bound: one
+	// wave's round waits for its loads)
+	for (uint32_t B = 0; B < total; B += CK_HALVES * WAVE) {
+		uint32_t r[CK_HALVES];
+		{
+			uint32_t ob[CK_HALVES];
+			int32_t lb[CK_HALVES], hb[CK_HALVES];
+			bool live[CK_HALVES];
 #pragma unroll
-		for (uint32_t s = WAVE / 2; s >= 1; s >>= 1) {
-			const uint32_t c = lo + s;
-			lo = lane_get(first, c) <= g ? c : lo;
+			for (uint32_t h = 0; h < CK_HALVES; ++h) {
+				const uint32_t g = B + WAVE * h + lane;
+				uint32_t lo = 0;
+#pragma unroll
+				for (uint32_t st = WAVE / 2; st >= 1; st >>= 1) {
+					const uint32_t c = lo + st;
+					lo = lane_get(first, c) <= g ? c : lo;
+				}
+				const uint32_t q = g - lane_get(first, lo);
+				const uint32_t pr = lane_get(prm, lo);
+				ob[h] = lane_get(base, lo) + 64u * q;
+				live[h] = g < total;
+				// the piece's byte window [lb, hb), relative to its start
+				lb[h] = (int32_t)(pr & 63u) - (int32_t)(64u * q);
+				hb[h] = (int32_t)(pr >> 6) - (int32_t)(64u * q);
+			}
+			u32x4 v[CK_HALVES][4];
+			uint32_t xh[CK_HALVES], xt[CK_HALVES];
+#pragma unroll
+			for (uint32_t h = 0; h < CK_HALVES; ++h) {
+#pragma unroll
+				for (int32_t k = 0; k < 4; ++k)   // only 16-B parts that reach into [from, to)
+					v[h][k] = __builtin_amdgcn_raw_buffer_load_b128(
+						rs, (live[h] && 16 * k < hb[h] && 16 * k + 16 > lb[h]) ? ob[h] + 16u * k
+													: OOB_OFF, 0, 0);
+				const bool ph = live[h] && lb[h] > 0 && (lb[h] & 3) != 0;
+				const bool pt = live[h] && hb[h] < 64 && (hb[h] & 3) != 0;
+				xh[h] = __builtin_amdgcn_raw_buffer_load_b32(
+					rs, ph ? ob[h] + (uint32_t)(lb[h] & ~3) : OOB_OFF, 0, 0);
+				xt[h] = __builtin_amdgcn_raw_buffer_load_b32(
+					rs, pt ? ob[h] + (uint32_t)(hb[h] & ~3) : OOB_OFF, 0, 0);
+			}
+#pragma unroll
+			for (uint32_t h = 0; h < CK_HALVES; ++h) {
+				uint64_t sm = (uint64_t)(xh[h] >> 16) +
+					      (xt[h] & ((1u << (8u * ((uint32_t)hb[h] & 3u))) - 1u));
+				// dword d is wholly inside iff lb <= 4d and 4d + 4 <= hb
+				const uint32_t lo4 = (uint32_t)max(lb[h], 0);
+				const int32_t sp = hb[h] - 4 - max(lb[h], 0);   // < 0: no whole dword
+#pragma unroll
+				for (uint32_t d = 0; d < 16; ++d) {
+					const bool in = live[h] && sp >= 0 && (4u * d - lo4) <= (uint32_t)sp;
+					sm += in ? v[h][d >> 2][d & 3u] : 0u;
+				}
+				// < 2^20 + 2^16
+				r[h] = (uint32_t)(sm & 0xffffu) + (uint32_t)(sm >> 16);
+			}
 		}
-		const uint32_t q = g - lane_get(first, lo);
-		const uint32_t pr = lane_get(prm, lo);
-		const uint32_t ob = lane_get(base, lo) + 64u * q;
-		const bool live = g < total;
-		// the piece's byte window [lb, hb), relative to its start
-		const int32_t lb = (int32_t)(pr & 63u) - (int32_t)(64u * q);
-		const int32_t hb = (int32_t)(pr >> 6) - (int32_t)(64u * q);
-		u32x4 v[4];
-#ifdef DIAG_CK_COALESCED
-		// diagnostic timing variant: load k of lane j reads part j & 3 of
-		// the round's piece 16 k + j / 4 (each load covers 16 whole pieces;
-		// the sums are wrong)
+		// prefix sums over the round's pieces (half h continues half h - 1)
+		uint32_t P[CK_HALVES], T = 0;
 #pragma unroll
-		for (uint32_t k = 0; k < 4; ++k) {
-			const uint32_t src = 16u * k + (lane >> 2);
-			const uint32_t o2 = lane_get(ob, src) + 16u * (lane & 3u);
-			v[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, lane_get(live ? 1u : 0u, src) ? o2 : OOB_OFF,
-								    0, 0);
+		for (uint32_t h = 0; h < CK_HALVES; ++h) {
+			P[h] = wave_scan_add(r[h], lane) + T;
+			T = (uint32_t)__builtin_amdgcn_readlane((int)P[h], WAVE - 1);
 		}
-#else
-#pragma unroll
-		for (int32_t k = 0; k < 4; ++k)   // only 16-B parts that reach into [from, to)
-			v[k] = __builtin_amdgcn_raw_buffer_load_b128(
-				rs, (live && 16 * k < hb && 16 * k + 16 > lb) ? ob + 16u * k : OOB_OFF, 0, 0);
-#endif
-		const bool ph = live && lb > 0 && (lb & 3) != 0;
-		const bool pt = live && hb < 64 && (hb & 3) != 0;
-		const uint32_t xh = __builtin_amdgcn_raw_buffer_load_b32(
-			rs, ph ? ob + (uint32_t)(lb & ~3) : OOB_OFF, 0, 0);
-		const uint32_t xt = __builtin_amdgcn_raw_buffer_load_b32(
-			rs, pt ? ob + (uint32_t)(hb & ~3) : OOB_OFF, 0, 0);
-		uint64_t s = (uint64_t)(xh >> 16) + (xt & ((1u << (8u * ((uint32_t)hb & 3u))) - 1u));
-		// dword d is wholly inside iff lb <= 4d and 4d + 4 <= hb
-		const uint32_t lo4 = (uint32_t)max(lb, 0);
-		const int32_t sp = hb - 4 - max(lb, 0);   // < 0: no whole dword
-#pragma unroll
-		for (uint32_t d = 0; d < 16; ++d) {
-			const bool in = live && sp >= 0 && (4u * d - lo4) <= (uint32_t)sp;
-			s += in ? v[d >> 2][d & 3u] : 0u;
-		}
-		// < 2^20 + 2^16
-		const uint32_t r = (uint32_t)(s & 0xffffu) + (uint32_t)(s >> 16);
-		const uint32_t P = wave_scan_add(r, lane);
-		// this lane's pieces in the round: lanes [a, e) of it
+		// this lane's pieces in the round: [a, e) of it
 		const uint32_t a = first > B ? first - B : 0u;
-		const uint32_t e = min(incl > B ? incl - B : 0u, (uint32_t)WAVE);
-		const uint32_t pe = lane_get(P, e > 0u ? e - 1u : 0u);
-		const uint32_t pa = lane_get(P, a > 0u ? a - 1u : 0u);
+		const uint32_t e = min(incl > B ? incl - B : 0u, (uint32_t)(CK_HALVES * WAVE));
+		const uint32_t ie = e > 0u ? e - 1u : 0u, ia = a > 0u ? a - 1u : 0u;
+		uint32_t pe = 0, pa = 0;
+#pragma unroll
+		for (uint32_t h = 0; h < CK_HALVES; ++h) {
+			const uint32_t xe = lane_get(P[h], ie & (WAVE - 1u));
+			const uint32_t xa = lane_get(P[h], ia & (WAVE - 1u));
+			pe = ie / WAVE == h ? xe : pe;
+			pa = ia / WAVE == h ? xa : pa;
+		}
 		acc += (e > a) ? pe - (a > 0u ? pa : 0u) : 0u;
 	}
 	return acc;
@@ -633,13 +698,24 @@ __device__ __forceinline__ uint32_t sctp_crc(const Pkt &k, __amdgpu_buffer_rsrc_
 }
 
 // a * b mod P in the reflected domain (zlib multmodp), branch-free
+// Five VALU operations per bit, one statement per bit: the compiler's
+// own lowering took seven and hoisted the 32 bit masks of `a` into 32 live
+// registers, which spilled the checksum kernels (v_bitop3_b32 0x78 = S0 ^
+// (S1 & S2)).
 __device__ __forceinline__ uint32_t crc_mulmod(uint32_t a, uint32_t b)
 {
 	uint32_t p = 0;
+	const uint32_t poly = 0x82F63B78u;
 #pragma unroll
 	for (int i = 31; i >= 0; --i) {
-		p ^= ((a >> i) & 1u) ? b : 0u;
-		b = (b >> 1) ^ ((b & 1u) ? 0x82F63B78u : 0u);
+		uint32_t m, t;
+		asm("v_bfe_i32 %[m], %[a], %[i], 1\n\t"
+		    "v_bitop3_b32 %[p], %[p], %[m], %[b] bitop3:0x78\n\t"
+		    "v_bfe_i32 %[t], %[b], 0, 1\n\t"
+		    "v_lshrrev_b32 %[b], 1, %[b]\n\t"
+		    "v_bitop3_b32 %[b], %[b], %[t], %[P] bitop3:0x78"
+		    : [p] "+v"(p), [b] "+v"(b), [m] "=&v"(m), [t] "=&v"(t)
+		    : [a] "v"(a), [i] "i"(i), [P] "s"(poly));
 	}
 	return p;
 }
@@ -657,31 +733,62 @@ __device__ __forceinline__ uint32_t wave_scan_xor(uint32_t v, uint32_t lane)
 	return v ^ (row >= 1u ? r0 : 0u) ^ (row >= 2u ? r1 : 0u) ^ (row >= 3u ? r2 : 0u);
 }
 
+// The register advanced over 16 / 32 zero bytes (tables s128 / s256 at S).
+__device__ __forceinline__ uint32_t crc_shift(const uint32_t *S, uint32_t v)
+{
+	return S[v & 0xffu] ^ S[256u + ((v >> 8) & 0xffu)] ^ S[512u + ((v >> 16) & 0xffu)] ^
+	       S[768u + (v >> 24)];
+}
+
+// Raw CRC-32C (init 0) of 64 bytes: four independent chains of four
+// slicing-by-4 steps (one per 16-B chunk), joined pairwise -- six dependent
+// LDS lookup levels instead of sixteen.
+__device__ __forceinline__ uint32_t crc_piece(const uint32_t *tab, const u32x4 v[4])
+{
+	uint32_t c[4];
+#pragma unroll
+	for (uint32_t i = 0; i < 4; ++i) {
+		uint32_t x = 0;
+#pragma unroll
+		for (uint32_t d = 0; d < 4; ++d)
+			x = crc32c_u32(tab, x, v[i][d]);
+		c[i] = x;
+	}
+	const uint32_t h0 = crc_shift(tab + CRC_S128, c[0]) ^ c[1];
+	const uint32_t h1 = crc_shift(tab + CRC_S128, c[2]) ^ c[3];
+	return crc_shift(tab + CRC_S256, h0) ^ h1;
+}
+
 // Wave-cooperative CRC-32C of the SCTP check (all 64 lanes active): lane f
 // asks (ask != 0) for the CRC over frame bytes [l4, len) of its frame (batch
 // offset boff) with the checksum field [l4 + 8, l4 + 12) taken as zero, init
-// ~0, inverted.  The bytes are cut into the nf = (len - l4) / 64 full 64-B
-// pieces counted from l4 and a last partial piece of r = (len - l4) % 64
-// bytes.  The full pieces of all lanes are dealt out 64 per round as in
-// ck_sum_wave (16-B loads from l4 on: no byte below l4 is ever read into a
-// CRC, and the checksum field is dword 2 of piece 0, so no masks).  CRC is
-// linear over GF(2): a lane computes the raw CRC (init 0) of its piece and
-// shifts it by the full pieces after it, x^(512 (nf - 1 - k)) (table z); the
-// frame's register is the XOR of its pieces' (prefix XOR over the round),
-// shifted once more by the r partial bytes (x^(8 r), table y), XOR the raw
-// CRC of the partial piece (its owner lane walks it: <= 15 words + 3 bytes),
-// plus the init's contribution ~0 * x^(8 (len - l4)).  Returns the finished
-// CRC for the asking lanes.
+// ~0, inverted.  The n = len - l4 bytes are cut into 64-B pieces counted from
+// l4: nf = n / 64 full ones and, when rr = n % 64 != 0, a last one of rr
+// bytes zero-padded to 64 (its 16-B parts past rr not loaded, the boundary
+// word masked).  The pieces of all lanes are numbered in lane order and dealt
+// out 64 per round as in ck_sum_wave (16-B loads from l4 on: no byte below l4
+// is ever read into a CRC, and the checksum field is dword 2 of piece 0).
+// CRC is linear over GF(2): a lane computes the raw CRC (init 0) of its
+// piece (crc_piece) and shifts it by the 64-B blocks after it, x^(512 (nf -
+// k)) (table z; the padded last piece counts as a block even when rr = 0);
+// the frame's register is the XOR of its pieces' (prefix XOR over the round)
+// = raw(message) x^(8 (64 - rr)), brought back by x^(-8 (64 - rr)) (table
+// yinv), plus the init's contribution ~0 x^(8 n) = y1[rr] z[nf].  One GF(2)
+// multiply per piece and two per frame.  (Round 3 had the last piece walked
+// by its owner lane, up to 18 dependent table steps after the rounds.)
+// Returns the finished CRC for the asking lanes.
 __device__ __forceinline__ uint32_t sctp_crc_wave(__amdgpu_buffer_rsrc_t rs, uint32_t boff,
 						  uint32_t l4, uint32_t len, uint32_t ask,
 						  uint32_t lane, const uint32_t *tab)
 {
-	const uint32_t *zt = tab + 1024u, *yt = zt + CRC_ZN;
+	const uint32_t *zt = tab + CRC_Z;
 	const uint32_t n = ask ? len - l4 : 0u, nf = n >> 6, rr = n & 63u;
-	const uint32_t incl = wave_scan_add(nf, lane);
-	const uint32_t first = incl - nf;
+	const uint32_t np = nf + (rr != 0u ? 1u : 0u);
+	const uint32_t incl = wave_scan_add(np, lane);
+	const uint32_t first = incl - np;
 	const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, WAVE - 1);
 	const uint32_t p0 = boff + l4;   // batch offset of the first L4 byte
+	const uint32_t fi = nf | (rr << 16);
 	uint32_t acc = 0;
 	for (uint32_t B = 0; B < total; B += WAVE) {
 		const uint32_t g = B + lane;
@@ -692,42 +799,25 @@ __device__ __forceinline__ uint32_t sctp_crc_wave(__amdgpu_buffer_rsrc_t rs, uin
 			lo = lane_get(first, c) <= g ? c : lo;
 		}
 		const uint32_t k = g - lane_get(first, lo);   // piece number from l4
-		const uint32_t fnf = lane_get(nf, lo);
+		const uint32_t f2 = lane_get(fi, lo), fnf = f2 & 0xffffu;
 		const uint32_t ob = lane_get(p0, lo) + 64u * k;
 		const bool live = g < total;
+		// bytes of the piece: 64, or the last piece's rr
+		const uint32_t vb = k < fnf ? 64u : f2 >> 16;
 		u32x4 v[4];
-#ifdef DIAG_CK_COALESCED
-#pragma unroll
-		for (uint32_t i = 0; i < 4; ++i) {
-			const uint32_t src = 16u * i + (lane >> 2);
-			const uint32_t o2 = lane_get(ob, src) + 16u * (lane & 3u);
-			v[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, lane_get(live ? 1u : 0u, src) ? o2 : OOB_OFF,
-								    0, 0);
-		}
-#else
 #pragma unroll
 		for (uint32_t i = 0; i < 4; ++i)
-			v[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, live ? ob + 16u * i : OOB_OFF, 0, 0);
-#endif
-		uint32_t crc = 0;
-#ifdef DIAG_CRC_NOCHAIN
-		// diagnostic timing variant: the words XORed, no table steps
-#pragma unroll
-		for (uint32_t d = 0; d < 16; ++d)
-			crc ^= v[d >> 2][d & 3];
-#else
+			v[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (live && 16u * i < vb) ? ob + 16u * i
+									     : OOB_OFF, 0, 0);
+		const uint32_t bm = (1u << (8u * (vb & 3u))) - 1u;
 #pragma unroll
 		for (uint32_t d = 0; d < 16; ++d) {
 			const uint32_t w = v[d >> 2][d & 3];
-			crc = crc32c_u32(tab, crc, (d == 2u && k == 0u) ? 0u : w);   // the checksum field
+			v[d >> 2][d & 3] = (d == 2u && k == 0u) ? 0u   // the checksum field
+				: (4u * d + 4u <= vb ? w : ((4u * d < vb) ? (w & bm) : 0u));
 		}
-#endif
-		// shift by the full pieces after this one
-#ifdef DIAG_CRC_NOMUL
-		const uint32_t r = live ? crc ^ zt[min(fnf - 1u - k, (uint32_t)CRC_ZN - 1u)] : 0u;
-#else
-		const uint32_t r = live ? crc_mulmod(crc, zt[min(fnf - 1u - k, (uint32_t)CRC_ZN - 1u)]) : 0u;
-#endif
+		const uint32_t crc = crc_piece(tab, v);
+		const uint32_t r = live ? crc_mulmod(crc, zt[fnf - k]) : 0u;
 		const uint32_t P = wave_scan_xor(r, lane);
 		const uint32_t a0 = first > B ? first - B : 0u;
 		const uint32_t e = min(incl > B ? incl - B : 0u, (uint32_t)WAVE);
@@ -735,46 +825,8 @@ __device__ __forceinline__ uint32_t sctp_crc_wave(__amdgpu_buffer_rsrc_t rs, uin
 		const uint32_t pa = lane_get(P, a0 > 0u ? a0 - 1u : 0u);
 		acc ^= (e > a0) ? (pe ^ (a0 > 0u ? pa : 0u)) : 0u;
 	}
-	// the full pieces sit rr bytes before the frame end
-	acc = (ask && nf) ? crc_mulmod(acc, yt[rr]) : 0u;
-	// the partial piece, walked by its owner: words, then 0-3 bytes
-#ifndef DIAG_CRC_NOTAIL
-	{
-		const uint32_t pb = p0 + 64u * nf;   // its first byte
-		u32x4 v[4];
-#pragma unroll
-		for (uint32_t i = 0; i < 4; ++i)
-			v[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (ask && 16u * i < rr) ? pb + 16u * i
-									     : OOB_OFF, 0, 0);
-		uint32_t crc = 0;
-#pragma unroll
-		for (uint32_t d = 0; d < 15; ++d) {
-			const uint32_t w = v[d >> 2][d & 3];
-			if (__ballot(ask && 4u * d + 4u <= rr) != 0ull) {
-				if (ask && 4u * d + 4u <= rr)
-					crc = crc32c_u32(tab, crc, (d == 2u && nf == 0u) ? 0u : w);
-			}
-		}
-		// the word holding the tail bytes (selects: no dynamic register index)
-		const uint32_t q = rr >> 2;
-		uint32_t wl = 0u;
-#pragma unroll
-		for (uint32_t d = 0; d < 16; ++d)
-			wl = d == q ? v[d >> 2][d & 3] : wl;
-#pragma unroll
-		for (uint32_t b = 0; b < 3; ++b) {
-			// a tail byte of the checksum field (frames of < 12 L4 bytes) is zero
-			const uint32_t o = 4u * q + b;
-			const bool in = ask && o < rr;
-			const uint32_t byte = (nf == 0u && o >= 8u && o < 12u) ? 0u : ((wl >> (8u * b)) & 0xffu);
-			crc = in ? crc32c_u8(tab, crc, byte) : crc;
-		}
-		acc ^= crc;
-	}
-#endif
-	// the init register ~0 shifted over the whole message
-	const uint32_t sh = crc_mulmod(zt[min(n >> 6, (uint32_t)CRC_ZN - 1u)], yt[n & 63u]);
-	return ~(acc ^ crc_mulmod(0xFFFFFFFFu, sh));
+	const uint32_t raw = crc_mulmod(acc, tab[CRC_YINV + 64u - rr]);
+	return ~(raw ^ crc_mulmod(tab[CRC_Y1 + rr], zt[nf]));
 }
 
 // _odp_packet_l4_chksum (odp_packet.c:2065-2138) for the lanes whose parse
@@ -817,14 +869,20 @@ __device__ __forceinline__ void l4_chksum(const Pkt &k, Parsed &p, uint32_t opt,
 			base = boff + p0;
 			prm = (l4 - p0) | ((len - p0) << 6);
 		}
+#ifndef DIAG_CK_NOSUM
 		s += ck_sum_wave(rs, base, prm, cnt, lane);
+#endif
 	}
 	bool bad = sum && ck_finalize(s) != 0xffffu;   // ~sum != 0
 	if (__ballot(kind == 3u) != 0ull) {
 		// frames with at most CRC_ZN 64-B pieces: the wave cooperates;
 		// longer (jumbo) ones: one lane walks its frame
 		const bool wv = kind == 3u && len - l4 < 64u * CRC_ZN;
+#ifdef DIAG_CK_NOSCTP
+		const uint32_t crc = 0u;
+#else
 		const uint32_t crc = sctp_crc_wave(rs, boff, l4, len, wv ? 1u : 0u, lane, crc_tab);
+#endif
 		if (wv)
 			bad = crc != r32(k, l4 + 8u);
 		if (__ballot(kind == 3u && !wv) != 0ull) {
@@ -832,6 +890,11 @@ __device__ __forceinline__ void l4_chksum(const Pkt &k, Parsed &p, uint32_t opt,
 				bad = sctp_crc(k, rs, boff, l4, crc_tab) != r32(k, l4 + 8u);
 		}
 	}
+#ifdef DIAG_CK_OK
+	// diagnostic timing variants: every L4 checksum passes, so variants
+	// that skip checksum work classify the same lanes downstream
+	bad = false;
+#endif
 	if (kind != 0u) {
 		p.flags |= F_L4CK_DONE;
 		if (bad) {
@@ -2160,7 +2223,7 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 	__shared__ uint32_t s_cnt[MAX_STATS_COS];
 	__shared__ uint32_t s_l4[256];
 	// CRC-32C slicing tables and piece shifts (pktin options)
-	__shared__ uint32_t s_crc[CK ? 1024 + CRC_ZN + 64 : 1];
+	__shared__ uint32_t s_crc[CK ? CRC_WORDS : 1];
 
 	const uint32_t lane = threadIdx.x & (WAVE - 1);
 	const uint32_t wave = threadIdx.x >> 6;
@@ -2251,9 +2314,10 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 	for (uint32_t i = threadIdx.x; i < 256u; i += NW * WAVE)
 		s_l4[i] = c_l4tab.v[i];
 	if constexpr (CK) {
-		for (uint32_t i = threadIdx.x; i < 1024u + CRC_ZN + 64u; i += NW * WAVE)
-			s_crc[i] = i < 1024u ? c_crc32c.t[i >> 8][i & 0xffu]
-				 : (i < 1024u + CRC_ZN ? c_crc32c.z[i - 1024u] : c_crc32c.y[i - 1024u - CRC_ZN]);
+		// Crc32cTab's words in order (CRC_* offsets)
+		const uint32_t *cw = reinterpret_cast<const uint32_t *>(&c_crc32c);
+		for (uint32_t i = threadIdx.x; i < CRC_WORDS; i += NW * WAVE)
+			s_crc[i] = cw[i];
 	}
 	for (uint32_t r = WIN / 4; r < WROWS; ++r)
 		W[r * RS + lane] = 0u;   // pad / zero rows: always zero
@@ -2656,13 +2720,25 @@ static inline const void *mi_kaddr(void (*k)(KArgs))
 	return reinterpret_cast<const void *>(k);
 }
 
+// `lds` caches the kernel's static LDS bytes (one per launch site): a launch
+// whose static + dynamic LDS exceeds the CU's 160 KiB fails with -E2BIG
+// instead of running with a hot-region copy past the allocation.
+#define MI_LDS_BYTES (160u * 1024u)
 static inline int mi_launch(const void *k, unsigned grid, unsigned block, size_t dyn, hipStream_t st,
-			    const KArgs &a)
+			    const KArgs &a, size_t *lds)
 {
-	if (grid == 0) {
+	size_t sl = __atomic_load_n(lds, __ATOMIC_RELAXED);
+	if (sl == ~(size_t)0) {
 		hipFuncAttributes fa;
-		return hipFuncGetAttributes(&fa, k) == hipSuccess ? 0 : -EIO;
+		if (hipFuncGetAttributes(&fa, k) != hipSuccess)
+			return -EIO;
+		sl = fa.sharedSizeBytes;
+		__atomic_store_n(lds, sl, __ATOMIC_RELAXED);
 	}
+	if (grid == 0)
+		return 0;
+	if (sl + dyn > MI_LDS_BYTES)
+		return -E2BIG;
 	void *args[] = { (void *)&a };
 	return hipLaunchKernel(k, dim3(grid), dim3(block), args, dyn, st) == hipSuccess ? 0 : -EIO;
 }
@@ -2675,7 +2751,8 @@ static inline int mi_launch(const void *k, unsigned grid, unsigned block, size_t
 #else
 #define MI_LAUNCH(K, grid, block, dyn, st, a)                                             \
 	do {                                                                               \
-		const int rc_ = mi_launch(mi_kaddr(K), grid, (unsigned)(block), dyn, st, a); \
+		static size_t lds_ = ~(size_t)0;                                           \
+		const int rc_ = mi_launch(mi_kaddr(K), grid, (unsigned)(block), dyn, st, a, &lds_); \
 		if (rc_)                                                                   \
 			return rc_;                                                        \
 	} while (0)
