@@ -1262,7 +1262,8 @@ int odp_amd_cls_all_cos_pooled(void)
 
 	pthread_mutex_lock(&G.lock);
 	for (uint32_t i = 0; G.init && i < G.max_cos; i++)
-		if (G.cos[i].valid) {
+		if (G.cos[i].valid && G.cos[i].action != ODP_COS_ACTION_DROP) {
+			/* (a drop CoS never takes a packet) */
 			any = 1;
 			if (G.cos[i].pool == ODP_POOL_INVALID)
 				all = 0;

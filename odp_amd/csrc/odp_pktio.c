@@ -59,7 +59,7 @@ enum { ST_OPENED = 0, ST_STARTED, ST_STOPPED };
 #define RX_BURST_DEFAULT 4096
 /* staging sets per pktio: one burst staged and classified, one whose GPU
  * delivery is in flight, one being staged */
-#define RX_SETS 3
+#define RX_SETS 4
 /* in-place loop bursts: offsets from the pinned arena's base stay below the
  * kernel's out-of-range offset */
 #define OOB_SPAN ((size_t)0xF0000000u)
@@ -2245,10 +2245,16 @@ static void rx_finish_start(rt_pktio_t *e, rx_set_t *s)
 static int pktio_recv(rt_pktio_t *e, odp_packet_t out[], int max_out)
 {
 	/* s: staged now; p: staged by the previous call (classified on the GPU
-	 * if it was left in flight); a: staged two calls ago (its GPU delivery
-	 * in flight if it was started) */
+	 * if it was left in flight); the older sets: GPU deliveries in flight,
+	 * a the oldest (started RX_SETS - 2 calls ago): a delivery (frame
+	 * copies over PCIe, ~100 us per 4096-frame burst) gets that many calls
+	 * of host work to hide behind before a call waits for it */
 	rx_set_t *s = &e->rs[e->cur], *p = &e->rs[(e->cur + RX_SETS - 1) % RX_SETS],
 		 *a = &e->rs[(e->cur + 1) % RX_SETS];
+	int older = 0;   /* deliveries in flight */
+
+	for (int k = 1; k <= RX_SETS - 2; k++)
+		older += e->rs[(e->cur + k) % RX_SETS].delivering;
 	const int pipe = e->cls_enabled && e->parse_layer != ODP_PROTO_LAYER_NONE &&
 			 rx_pipeline();
 	uint32_t burst = rx_burst();
@@ -2278,7 +2284,7 @@ static int pktio_recv(rt_pktio_t *e, odp_packet_t out[], int max_out)
 	uint64_t t1 = prof_ns();
 
 	e->prof[0] += t1 - t0;
-	if (n < 0 && !p->pending && !a->delivering)
+	if (n < 0 && !p->pending && !older)
 		return n;
 	s->n = n > 0 ? n : 0;
 	if (n > 0) {
@@ -2299,6 +2305,13 @@ static int pktio_recv(rt_pktio_t *e, odp_packet_t out[], int max_out)
 			rx_finish_start(e, p);
 		e->cur = (e->cur + 1) % RX_SETS;
 		return num_rx;
+	}
+	/* the rest in arrival order: deliveries still in flight, p, s */
+	for (int k = 2; k <= RX_SETS - 2; k++) {
+		rx_set_t *b = &e->rs[(e->cur + k) % RX_SETS];
+
+		if (b->delivering)
+			num_rx += rx_dlv_end(e, b, out + num_rx, max_out - num_rx);
 	}
 	if (p->pending)
 		num_rx += rx_finish(e, p, out + num_rx, max_out - num_rx);

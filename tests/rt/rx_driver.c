@@ -228,7 +228,7 @@ static void print_ev(const char *q, odp_event_t ev)
 }
 
 static int count_only;
-static uint64_t delivered;
+static uint64_t delivered, recv_ns, drain_ns;
 
 static void print_pkt(const char *q, odp_packet_t pkt)
 {
@@ -431,7 +431,12 @@ again:
 		const char *sw = getenv("RX_SWITCH_RULES");
 
 		while (idle < 3) {
+			odp_time_t t0 = odp_time_local();
+
 			n = odp_pktin_recv(inq, pk, 512);
+			odp_time_t t1 = odp_time_local();
+
+			recv_ns += odp_time_diff_ns(t1, t0);
 			if (sw) {
 				FILE *f = fopen(sw, "r");
 
@@ -456,6 +461,7 @@ again:
 					for (int i = 0; i < m; i++)
 						print_ev("-", ev[i]);
 			}
+			drain_ns += odp_time_diff_ns(odp_time_local(), t1);
 			idle = (n == 0 && odp_amd_pktio_rx_idle(pktio) == 1) ? idle + 1 : 0;
 		}
 		/* classified packets went to CoS queues: drain them */
@@ -501,9 +507,12 @@ again:
 				usleep(2000);   /* let the aggregators' max_tmo_ns pass */
 		}
 	}
-	if (count_only)
+	if (count_only) {
 		printf("R %" PRIu64 " %" PRIu64 "\n", delivered,
 		       timed_ns + odp_time_diff_ns(odp_time_local(), t_start));
+		/* direct mode: time in odp_pktin_recv vs draining the CoS queues */
+		fprintf(stderr, "RXLOOP recv_ns %" PRIu64 " drain_ns %" PRIu64 "\n", recv_ns, drain_ns);
+	}
 	odp_pktio_stats_t st;
 
 	odp_pktio_stats(pktio, &st);

@@ -22,12 +22,12 @@ PY
 run() {  # name mode env...
   local name=$1 m=$2; shift 2
   env "$@" ODP_AMD_RX_PROF=1 RX_COUNT_ONLY=1 timeout -k 10 120 tests/_bin/rx_driver pcap:in=$OUT/in.pcap:loops=${LOOPS:-10} $OUT/rules.txt $m 4 0 1 > $OUT/$name.txt 2>&1 || { tail $OUT/$name.txt; exit 1; }
-  echo "$name: $(grep -E '^(R|S|RXPROF) ' $OUT/$name.txt | sed 's/pcap:in=[^ ]* //' | tr '\n' ' ')"
+  echo "$name: $(grep -E '^(R|S|RXPROF|RXLOOP) ' $OUT/$name.txt | sed 's/pcap:in=[^ ]* //' | tr '\n' ' ')"
 }
 runloop() {  # name env...
   local name=$1; shift
   env "$@" ODP_AMD_RX_PROF=1 RX_COUNT_ONLY=1 RX_LOOP_ROUNDS=60 RX_POOL_NUM=65536 timeout -k 10 120 tests/_bin/rx_driver loop $OUT/rules.txt direct 4 0 1 $OUT/in_loop.pcap > $OUT/$name.txt 2>&1 || { tail $OUT/$name.txt; exit 1; }
-  echo "$name: $(grep -E '^(R|S|RXPROF loop) ' $OUT/$name.txt | tr '\n' ' ')"
+  echo "$name: $(grep -E '^(R|S|RXPROF loop|RXLOOP) ' $OUT/$name.txt | tr '\n' ' ')"
 }
 LOOPS=${3:-10}
 FRAMES=${2:-200000}
