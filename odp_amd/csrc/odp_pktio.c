@@ -59,7 +59,11 @@ enum { ST_OPENED = 0, ST_STARTED, ST_STOPPED };
 #define RX_BURST_DEFAULT 4096
 /* staging sets per pktio: one burst staged and classified, one whose GPU
  * delivery is in flight, one being staged */
-#define RX_SETS 4
+/* receive pipeline depth (pktio_recv): classifications and GPU deliveries
+ * in flight */
+#define RX_CLS_DEPTH 1
+#define RX_DLV_DEPTH 2
+#define RX_SETS (1 + RX_CLS_DEPTH + RX_DLV_DEPTH)
 /* in-place loop bursts: offsets from the pinned arena's base stay below the
  * kernel's out-of-range offset */
 #define OOB_SPAN ((size_t)0xF0000000u)
@@ -144,7 +148,7 @@ typedef struct {
 	 * previous one is delivered (pipelined receive) */
 	rx_set_t rs[RX_SETS];
 	int cur;                /* set the next burst is staged into */
-	uint64_t prof[12];      /* ODP_AMD_RX_PROF: ns staging / classifying / delivering, bursts,
+	uint64_t prof[14];      /* ODP_AMD_RX_PROF: ns staging / classifying / delivering, bursts,
 				 * then of delivering: ns preparing / enqueueing, TSC ticks in
 				 * packet allocation / frame copies; GPU delivery: ns deciding +
 				 * taking packets + entries, ns in the delivery kernel (submit to
@@ -827,9 +831,10 @@ int odp_pktio_close(odp_pktio_t h)
 		fprintf(stderr, "RXPROF %s bursts %" PRIu64 " stage_ns %" PRIu64 " classify_ns %" PRIu64
 			" deliver_ns %" PRIu64 " (prepare_ns %" PRIu64 " enqueue_ns %" PRIu64
 			" alloc_tsc %" PRIu64 " copy_tsc %" PRIu64 ") gpu_bursts %" PRIu64
-			" (decide_ns %" PRIu64 " kernel_ns %" PRIu64 " enqueue_ns %" PRIu64 ")\n", e->name,
+			" (decide_ns %" PRIu64 " submit_ns %" PRIu64 " kernel_ns %" PRIu64 " enqueue_ns %" PRIu64
+			") cls_submit_ns %" PRIu64 "\n", e->name,
 			e->prof[3], e->prof[0], e->prof[1], e->prof[2], e->prof[4], e->prof[5], e->prof[6],
-			e->prof[7], e->prof[11], e->prof[8], e->prof[9], e->prof[10]);
+			e->prof[7], e->prof[11], e->prof[8], e->prof[12], e->prof[9], e->prof[10], e->prof[13]);
 	if (e->inq != ODP_QUEUE_INVALID) {
 		odp_event_t ev[64];
 		int n;
@@ -2031,7 +2036,10 @@ static int rx_dlv_start(rt_pktio_t *e, rx_set_t *s, rx_cnt_t *c)
 		a.perm = s->perm;
 		a.gcnt = s->gcnt;
 		s->dticket = 0;
+		const uint64_t ts0 = prof_ns();
 		int rc = odp_amd_cls_deliver(e->hdl, &a, &s->dticket);
+
+		e->prof[12] += prof_ns() - ts0;
 
 		if (rc) {
 			s->dticket = 0;
@@ -2236,25 +2244,34 @@ static void rx_finish_start(rt_pktio_t *e, rx_set_t *s)
 	(void)rx_finish_host(e, s, &c, NULL, 0, t2);
 }
 
-/* One receive call.  With the classifier enabled, a burst whose successor is
- * already waiting at the driver is left in flight on the GPU while the
- * previous burst is delivered (one burst of latency, none when the driver
- * has nothing more: a call always delivers everything that was ready).
- * Unclassified packets are returned in out[] (at most max_out); classified
- * ones are enqueued to their CoS queues. */
+/* Set of age k: staged k calls ago (age 0: this call). */
+static rx_set_t *rx_age(rt_pktio_t *e, int k)
+{
+	return &e->rs[(e->cur + RX_SETS - k) % RX_SETS];
+}
+
+/* One receive call.  With the classifier enabled and more frames waiting at
+ * the driver, bursts stream through RX_SETS sets by age: staged and
+ * submitted for classification (age 0), classification in flight (ages 1 ..
+ * RX_CLS_DEPTH), decided from their records and GPU delivery started (age
+ * RX_CLS_DEPTH), delivery in flight (older), enqueued (the oldest).  Each
+ * GPU step then has that many calls of host work to run behind before a
+ * call waits for it (a delivery copies ~1.5 MB of frames over PCIe per
+ * 4096-frame burst).  A call with nothing more at the driver delivers
+ * everything, oldest first.  Unclassified packets are returned in out[] (at
+ * most max_out); classified ones are enqueued to their CoS queues. */
 static int pktio_recv(rt_pktio_t *e, odp_packet_t out[], int max_out)
 {
-	/* s: staged now; p: staged by the previous call (classified on the GPU
-	 * if it was left in flight); the older sets: GPU deliveries in flight,
-	 * a the oldest (started RX_SETS - 2 calls ago): a delivery (frame
-	 * copies over PCIe, ~100 us per 4096-frame burst) gets that many calls
-	 * of host work to hide behind before a call waits for it */
-	rx_set_t *s = &e->rs[e->cur], *p = &e->rs[(e->cur + RX_SETS - 1) % RX_SETS],
-		 *a = &e->rs[(e->cur + 1) % RX_SETS];
-	int older = 0;   /* deliveries in flight */
+	rx_set_t *s = rx_age(e, 0);
+	long pending_n = 0;   /* frames staged, not yet taken from pools */
+	int in_flight = 0;
 
-	for (int k = 1; k <= RX_SETS - 2; k++)
-		older += e->rs[(e->cur + k) % RX_SETS].delivering;
+	for (int k = 1; k < RX_SETS; k++) {
+		const rx_set_t *o = rx_age(e, k);
+
+		pending_n += o->pending ? (long)o->n : 0;
+		in_flight |= o->pending || o->delivering;
+	}
 	const int pipe = e->cls_enabled && e->parse_layer != ODP_PROTO_LAYER_NONE &&
 			 rx_pipeline();
 	uint32_t burst = rx_burst();
@@ -2266,14 +2283,14 @@ static int pktio_recv(rt_pktio_t *e, odp_packet_t out[], int max_out)
 		burst = (uint32_t)max_out;
 	if (e->drv == DRV_PCAP) {
 		/* pcap frames become packets of the pktio's pool at delivery: stage
-		 * no more than the pool can still hold after the burst in flight,
+		 * no more than the pool can still hold after the bursts in flight,
 		 * so a packet allocation never fails on a staged frame (frames not
 		 * staged stay in the store for the next call; the reference instead
 		 * consumes the frame and stops on a failed allocation, pcap.c:324-327) */
 		/* (frames that all go to CoS with pools of their own never take a
 		 * packet of the pktio's pool: no bound then) */
 		if (rt_pool(e->pool) && !(e->cls_enabled && odp_amd_cls_all_cos_pooled())) {
-			long room = (long)rt_pool_avail(e->pool) - (p->pending ? (long)p->n : 0);
+			long room = (long)rt_pool_avail(e->pool) - pending_n;
 
 			if (room < (long)burst)
 				burst = room > 0 ? (uint32_t)room : 0u;
@@ -2284,7 +2301,7 @@ static int pktio_recv(rt_pktio_t *e, odp_packet_t out[], int max_out)
 	uint64_t t1 = prof_ns();
 
 	e->prof[0] += t1 - t0;
-	if (n < 0 && !p->pending && !older)
+	if (n < 0 && !in_flight)
 		return n;
 	s->n = n > 0 ? n : 0;
 	if (n > 0) {
@@ -2293,28 +2310,31 @@ static int pktio_recv(rt_pktio_t *e, odp_packet_t out[], int max_out)
 			n = 0;
 		e->prof[1] += prof_ns() - t1;
 	}
-	/* bursts are delivered in arrival order: a, then p, then s */
-	if (a->delivering)
-		num_rx += rx_dlv_end(e, a, out, max_out);
-	/* only a burst really in flight waits (a multi-GPU pktio's submit
+	/* bursts are delivered in arrival order: the oldest first */
+	rx_set_t *z = rx_age(e, RX_SETS - 1);
+
+	if (z->delivering)
+		num_rx += rx_dlv_end(e, z, out, max_out);
+	/* only a burst really in flight streams (a multi-GPU pktio's submit
 	 * completes before it returns: ticket 0) */
 	if (n > 0 && pipe && s->ticket && rx_more(e)) {
-		/* streaming: p's GPU delivery runs while the next call stages and
-		 * classifies, s stays in flight; the next call stages into a */
-		if (p->pending)
-			rx_finish_start(e, p);
+		rx_set_t *q = rx_age(e, RX_CLS_DEPTH);
+
+		if (q->pending)
+			rx_finish_start(e, q);
 		e->cur = (e->cur + 1) % RX_SETS;
 		return num_rx;
 	}
-	/* the rest in arrival order: deliveries still in flight, p, s */
-	for (int k = 2; k <= RX_SETS - 2; k++) {
-		rx_set_t *b = &e->rs[(e->cur + k) % RX_SETS];
+	/* the rest in arrival order: deliveries in flight, then the bursts
+	 * still pending, then s */
+	for (int k = RX_SETS - 2; k >= 1; k--) {
+		rx_set_t *b = rx_age(e, k);
 
 		if (b->delivering)
 			num_rx += rx_dlv_end(e, b, out + num_rx, max_out - num_rx);
+		if (b->pending)
+			num_rx += rx_finish(e, b, out + num_rx, max_out - num_rx);
 	}
-	if (p->pending)
-		num_rx += rx_finish(e, p, out + num_rx, max_out - num_rx);
 	if (n > 0)
 		num_rx += rx_finish(e, s, out + num_rx, max_out - num_rx);
 	return num_rx;
