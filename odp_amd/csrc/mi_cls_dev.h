@@ -148,8 +148,19 @@ __device__ __forceinline__ uint32_t r32(const Pkt &k, uint32_t o)
 	uint32_t v = __builtin_amdgcn_alignbyte(k.w[(i + 1) * RS], k.w[i * RS], o & 3u);
 	const bool far = o + 4u > k.win;
 	if (__ballot(far) != 0ull) {
-		if (far)
-			v = rb(k, o) | (rb(k, o + 1) << 8) | (rb(k, o + 2) << 16) | (rb(k, o + 3) << 24);
+		if (far) {
+			// two dword loads from HBM (the dwords that start inside the
+			// frame: they end inside its 16-B rounding, the batch contract),
+			// funnel-shifted, the bytes past the frame zeroed.  Frames may
+			// start at any byte: the dword loads are unaligned then, which
+			// gfx950 serves.
+			const uint32_t a = o & ~3u;
+			const uint32_t w0 = a < k.len ? *(const uint32_t *)(k.g + a) : 0u;
+			const uint32_t w1 = a + 4u < k.len ? *(const uint32_t *)(k.g + a + 4u) : 0u;
+			const uint32_t keep = k.len > o ? min(k.len - o, 4u) : 0u;
+			v = __builtin_amdgcn_alignbyte(w1, w0, o & 3u);
+			v = keep >= 4u ? v : (v & ((1u << (8u * keep)) - 1u));
+		}
 	}
 	return v;
 }
