@@ -7,6 +7,7 @@ seeded inputs.
 import numpy as np
 import pytest
 
+from odp_amd import cls
 from odp_amd import pktgen as pg
 from odp_amd import rules as R
 from tests import refcases as RC
@@ -196,6 +197,90 @@ def test_joint_direct_tree_levels(built, gpu, leaf_kind, engine):
     got = both(prog, b, what=f"joint {leaf_kind}", engine=engine)
     s = summary(got)
     assert s["enq"] > 0 and s["cos_drop"] > 0
+
+
+def _joint_bitmap_tree(rng, n, pair):
+    """Default CoS -> 6 VLAN_ID_0 rules -> 6 mid CoS; every mid CoS has 10
+    rules over the same two key classes (a joint bitmap group): some rules
+    constrain one class, some both, in a different order per CoS, with
+    repeated values, so first-match order matters.  pair = the second class:
+    "dport" (merged UDP/TCP ports, one-word key, CoS slot in free bits) or
+    "sip6" (SIP6 /48, a two-word key: the slot appended)."""
+    prog = [R.cos("default", queue=1)]
+    mids = list(range(1, 7))
+    prog += [R.cos(f"mid{i}", queue=10 + i) for i in range(6)]
+    leaves = list(range(7, 27))
+    prog += [R.cos(f"leaf{i}", queue=50 + i, action=1 if i == 19 else 0) for i in range(20)]
+    prog.append(("default", 0))
+    vids = [300 + 5 * i for i in range(6)]
+    for i in range(6):
+        prog.append(("pmr", [R.t_be16(R.PMR_VLAN_ID_0, vids[i], 0x0FFF)], 0, mids[i], 0))
+    dips = [(10 << 24) | (k << 8) for k in range(5)]       # /24 prefixes
+    seconds = list(range(4))
+    rules = {}
+    for i in range(6):
+        rs = []
+        for j in range(10):
+            kind = (i + j) % 3   # 0: DIP only, 1: second only, 2: both
+            d, q = int(rng.integers(0, 5)), int(rng.integers(0, 4))
+            terms = []
+            if kind in (0, 2):
+                terms.append(R.t_ip4(R.PMR_DIP_ADDR, dips[d].to_bytes(4, "big"), 24))
+            if kind in (1, 2):
+                if pair == "dport":
+                    terms.append(R.t_be16(R.PMR_UDP_DPORT if q % 2 else R.PMR_TCP_DPORT,
+                                          7000 + 13 * q + i))
+                else:
+                    a6 = bytes([0x20, 0x01, 0x0d, 0xb8, i, q]) + bytes(10)
+                    terms.append(R.t_ip6(R.PMR_SIP6_ADDR, a6, 48))
+            prog.append(("pmr", terms, mids[i], leaves[(7 * i + j) % 20], (i * 32 + j) & 0xFFFF))
+            rs.append((kind, d, q))
+        rules[i] = rs
+    i = rng.integers(0, 6, n)
+    d = rng.integers(0, 6, n)          # 5: no DIP rule's prefix
+    q = rng.integers(0, 5, n)          # 4: no second-class value
+    ipver = np.full(n, 6 if pair == "sip6" else 4)
+    proto = np.where(q % 2 == 1, pg.IPPROTO_UDP, pg.IPPROTO_TCP)
+    dip4 = ((10 << 24) | (d << 8) | rng.integers(0, 256, n)).astype(np.uint64)
+    dport = np.where(q < 4, 7000 + 13 * q + i, rng.integers(1, 65535, n))
+    sip6 = rng.integers(0, 256, (n, 16)).astype(np.uint8)
+    if pair == "sip6":
+        sip6[:, :4] = [0x20, 0x01, 0x0d, 0xb8]
+        sip6[:, 4] = i
+        sip6[:, 5] = np.where(q < 4, q, 200)
+    vid0 = np.where(rng.random(n) < 0.9, np.array(vids)[i], 999)
+    b = pg.build_batch(np.where(rng.random(n) < 0.7, 60, 300), ipver=ipver, l4proto=proto,
+                       sip4=rng.integers(0, 2 ** 32, n).astype(np.uint64), dip4=dip4, sip6=sip6,
+                       dip6=rng.integers(0, 256, (n, 16)).astype(np.uint8),
+                       sport=rng.integers(1, 65535, n), dport=dport,
+                       ntags=np.where(rng.random(n) < 0.2, 2, 1), vid0=vid0,
+                       vid1=rng.integers(1, 4095, n), seed=11)
+    return b, prog
+
+
+@pytest.mark.parametrize("engine", ["auto", "nojoint", "wpb4", "linear"])
+@pytest.mark.parametrize("pair", ["dport", "sip6"])
+def test_joint_bitmap_tree_levels(built, gpu, pair, engine):
+    """A tree level whose CoS have bitmap blocks over the same two classes
+    is one joint bitmap group (per class one (key, CoS) table; the group's
+    alive rows, miss rows and result arrays per CoS slot): every record
+    bit-exact against the oracle, with and without joint tables.  (IPv6
+    traffic for the SIP6 pair: the DIP class is then absent, the rules that
+    need it never hold.)"""
+    rng = np.random.default_rng({"dport": 21, "sip6": 22}[pair])
+    b, prog = _joint_bitmap_tree(rng, 30_000, pair)
+    c = cls.Classifier(gpu=0)
+    try:
+        c.apply(prog)
+        info = c.program_info()
+    finally:
+        c.close()
+    assert info["tree"] and info["bitmap"] == 6, info
+    if engine == "auto":
+        assert info["joint_bitmap"] == 6, info
+    got = both(prog, b, what=f"joint bitmap {pair}", engine=engine)
+    s = summary(got)
+    assert s["enq"] > 0
 
 
 def test_config2_tree_equals_flat(built, gpu):
