@@ -1217,6 +1217,12 @@ static int stage_frames(rt_pktio_t *e, rx_set_t *s, uint32_t max)
 			pinned_of[k] = rp && rp->pinned;
 		}
 
+		/* header prefetch distance (ODP_AMD_LOOP_PF, A/B; 16 -> 96: loop receive
+		 * 17.5 -> 20.0 Mpkt/s, profiles/r04pf_loop_prefetch_ab.txt) */
+		static int pf = -1;
+
+		if (pf < 0)
+			pf = getenv("ODP_AMD_LOOP_PF") ? atoi(getenv("ODP_AMD_LOOP_PF")) : 96;
 		while (n < max) {
 			odp_event_t *ev = (odp_event_t *)(void *)(s->pk + n);
 			int want = (int)(max - n);
@@ -1225,9 +1231,10 @@ static int stage_frames(rt_pktio_t *e, rx_set_t *s, uint32_t max)
 			if (got <= 0)
 				break;
 			for (int i = 0; i < got; i++) {
-				if (i + 16 < got) {   /* both header lines (the sender wrote them) */
-					const uint8_t *nh = (const uint8_t *)rt_pkt_hdr(odp_packet_from_event(ev[i + 16]));
+				if (i + pf < got) {   /* both header lines (the sender wrote them) */
+					const uint8_t *nh = (const uint8_t *)rt_pkt_hdr(odp_packet_from_event(ev[i + pf]));
 
+					__builtin_prefetch(nh);
 					__builtin_prefetch(nh + 64);
 				}
 				odp_packet_t p = odp_packet_from_event(ev[i]);
