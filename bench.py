@@ -363,11 +363,16 @@ def cpu_baseline(prog, batch, seconds):
                       f"slices per thread"}
 
 
-def load_pmc(cfg, n):
+def load_pmc(cfg, n, name=None):
+    """The committed PMC summary of a workload (profiles/pmc_traffic.json,
+    written by tools/pmc_summary.py); name: an extra's own key (e.g.
+    config3_generic), else the config's workload name."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
             d = json.load(f)
+        if name:
+            return d.get(f"{name}_n{n}")
         return d.get(f"{WORKLOAD[cfg]}_n{n}") or d.get(f"config{cfg}_n{n}")
     except (OSError, ValueError, KeyError):
         return None
@@ -389,9 +394,28 @@ def issue_roof(kms, pmc):
                     f"{(pmc or {}).get('source')}"}
 
 
-def bench_cfg(cls, cfg, a, dev, local, steps, warmup, pktin_opt=0, parity=True, full_bytes=False):
+def bench_cfg(cls, cfg, a, dev, local, steps, warmup, pktin_opt=0, parity=True, full_bytes=False,
+              env=None, name=None):
     """Time one extra configuration (single stream and two streams), check
-    its records against the oracle."""
+    its records against the oracle.  env: library knobs set for this entry
+    only (e.g. MI_CLS_JIT=0: the generic kernels)."""
+    env = env or {}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        e = _bench_cfg(cls, cfg, a, dev, local, steps, warmup, pktin_opt, parity, full_bytes, name)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    if env:
+        e["env"] = env
+    return e
+
+
+def _bench_cfg(cls, cfg, a, dev, local, steps, warmup, pktin_opt, parity, full_bytes, name):
     import numpy as np
     from odp_amd import pktgen as pg, rules as R
     log(f"extra {WORKLOAD[cfg]}{' pktin_opt' if pktin_opt else ''}: workload")
@@ -426,7 +450,7 @@ def bench_cfg(cls, cfg, a, dev, local, steps, warmup, pktin_opt=0, parity=True, 
          "mpkts_per_s_2streams": round(b2.n * steps / w2 / 1e6, 2),
          "kernel_ms": round(k1, 5), "bytes_per_launch": nbytes,
          "roofline_frac": round(nbytes / (k1 * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)}
-    pmc = load_pmc(cfg, b2.n) if not pktin_opt else None
+    pmc = load_pmc(cfg, b2.n, name) if not pktin_opt else None
     if pmc:
         e["traffic"] = pmc.get("hbm_bytes_per_launch")
     if pmc:
@@ -470,6 +494,14 @@ def run_extras(a, dev, local):
             continue
         extra[WORKLOAD[cfg]] = bench_cfg(cls, cfg, a, dev, local, k_steps, 3,
                                          parity=not a.no_parity)
+    # what an application gets on the generic kernels: right after a rule
+    # change (the specialised kernel compiles in the background for 1-4 s)
+    # or without the compiler (MI_CLS_JIT=0); config 5 on the generic tree
+    # kernel instead of its tree plan (MI_CLS_NO_PLAN=1)
+    extra["config3_generic"] = bench_cfg(cls, 3, a, dev, local, k_steps, 3, parity=not a.no_parity,
+                                         env={"MI_CLS_JIT": "0"}, name="config3_generic")
+    extra["config5_generic"] = bench_cfg(cls, 5, a, dev, local, k_steps, 3, parity=not a.no_parity,
+                                         env={"MI_CLS_NO_PLAN": "1"}, name="config5_generic")
     # pktin checksum validation (IPv4 header, UDP/TCP sums over the whole
     # frame): config 3 IMIX with valid checksums; the kernel reads every
     # frame byte, so the bytes are frame + 22 B
@@ -505,6 +537,42 @@ def extras_child(a):
         return {"error": "extras process timed out (900 s)"}
     finally:
         os.unlink(path)
+
+
+def dist_init_kwargs(backend, local):
+    """torch.distributed.init_process_group arguments of one rank: RCCL
+    ("nccl") binds the rank's process group to its own device (device_id =
+    cuda:LOCAL_RANK, so the one reduction per run never lands on another
+    rank's GPU); gloo (CPU rehearsal) takes no device."""
+    import torch
+    if backend == "nccl":
+        return {"backend": "nccl", "device_id": torch.device(f"cuda:{local}")}
+    return {"backend": backend}
+
+
+def reduce_ranks(dist, red_dev, wall, n, kms, bytes_launch, parity):
+    """The multi-rank reductions of one timed run (no data-path collective:
+    these are the only collectives).  Returns the max wall time over ranks,
+    the packets all ranks classified per step, every rank's kernel_ms and
+    algorithmic bytes per launch (rank order), the aggregate roofline
+    achieved = sum of the ranks' bytes / the slowest rank's kernel time
+    (GB/s), and parity AND-ed over the ranks (None if no rank checked)."""
+    import torch
+    world = dist.get_world_size()
+    mine = torch.tensor([wall, float(n), kms, float(bytes_launch),
+                         -1.0 if parity is None else float(bool(parity))],
+                        dtype=torch.float64, device=red_dev)
+    allv = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(allv, mine)
+    rows = [[float(x) for x in t.cpu().tolist()] for t in allv]
+    walls = [r[0] for r in rows]
+    k = [r[2] for r in rows]
+    par = [r[4] for r in rows]
+    return {"wall": max(walls), "packets": int(sum(r[1] for r in rows)),
+            "kernel_ms": [round(x, 5) for x in k],
+            "bytes_per_launch": [int(r[3]) for r in rows],
+            "achieved_gbs": sum(r[3] for r in rows) / (max(k) * 1e-3) / 1e9,
+            "parity": None if all(p < 0 for p in par) else all(p == 1.0 for p in par)}
 
 
 def launch_ranks(n):
@@ -550,10 +618,7 @@ def main():
     backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
     if dist_on:
         torch.cuda.set_device(local)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-        else:
-            dist.init_process_group(backend)
+        dist.init_process_group(**dist_init_kwargs(backend, local))
     dev = torch.device(f"cuda:{local}")
 
     from odp_amd import cls, rules as R
@@ -598,24 +663,28 @@ def main():
                                    a.streams)
     launch = c.last_launch()
     red_dev = dev if backend == "nccl" else torch.device("cpu")   # where reductions run
-    if dist_on:
-        t = torch.tensor([wall], dtype=torch.float64, device=red_dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall = float(t.item())
-    if dist_on:
-        tn = torch.tensor([batch.n], dtype=torch.float64, device=red_dev)
-        dist.all_reduce(tn, op=dist.ReduceOp.SUM)
-        total_pkts = int(tn.item()) * a.steps
-    else:
-        total_pkts = batch.n * a.steps
-    value = total_pkts / wall / 1e6
     # with checksum options the kernel reads every frame byte
     bytes_launch = batch.header_bytes() if not a.pktin_opt else \
         int(batch.len.astype("int64").sum()) + 22 * batch.n
-    achieved = bytes_launch / (kms * 1e-3) / 1e9
+    out = records(t_out, batch.n).copy()
+    parity = None
+    if not a.no_parity and not a.timed_only:
+        # every rank checks its own shard: all of its records bit-exact vs the oracle
+        log("oracle parity")
+        parity = oracle_parity(prog, batch, out, pktin_opt=a.pktin_opt)
+    ranks = None
+    if dist_on:
+        ranks = reduce_ranks(dist, red_dev, wall, batch.n, kms, bytes_launch, parity)
+        wall = ranks["wall"]
+        total_pkts = ranks["packets"] * a.steps
+        parity = ranks["parity"]
+        achieved = ranks["achieved_gbs"]
+    else:
+        total_pkts = batch.n * a.steps
+        achieved = bytes_launch / (kms * 1e-3) / 1e9
+    value = total_pkts / wall / 1e6
     res = None
     if rank == 0:
-        out = records(t_out, batch.n).copy()
         pmc = load_pmc(a.config, batch.n)
         line = {
             "metric": "Mpkts/s classified device-resident",
@@ -643,14 +712,21 @@ def main():
                          "kernel": "mi_cls_kernel" + (" (program-specialised)" if spec and
                                                        not a.pktin_opt else ""),
                          "launch": launch,
-                         "kernel_ms": round(kms, 5),
+                         "kernel_ms": round(max(ranks["kernel_ms"]) if ranks else kms, 5),
                          "bytes_per_launch": bytes_launch,
                          "traffic_source": (pmc or {}).get("source")},
         }
-        if not a.no_parity and not a.timed_only:
-            # this rank's records, every one bit-exact vs the oracle
-            log("oracle parity")
-            line["parity_vs_oracle"] = oracle_parity(prog, batch, out, pktin_opt=a.pktin_opt)
+        if ranks:
+            # aggregate roofline: every rank's algorithmic bytes over the
+            # slowest rank's kernel time, against world x the HBM peak
+            line["roofline"].update(
+                frac=round(achieved / (HBM_PEAK_GBS * world), 5), peak=HBM_PEAK_GBS * world,
+                per_rank_kernel_ms=ranks["kernel_ms"],
+                per_rank_bytes_per_launch=ranks["bytes_per_launch"],
+                aggregate="sum of the ranks' bytes per launch / the slowest rank's kernel_ms")
+        if parity is not None:
+            # AND over every rank's shard (each checked against the oracle)
+            line["parity_vs_oracle"] = parity
         if world == 1 and not a.timed_only:
             if pmc:
                 line["issue"] = issue_roof(kms, pmc)

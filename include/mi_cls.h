@@ -361,6 +361,9 @@ typedef struct mi_cls_dlv {
 #define MI_CLS_DLV_COPY  0x02u  /* copy the frame into meta + data_from_meta    */
 #define MI_CLS_DLV_CLS   0x04u  /* classifier on: cos / cls_mark / dst_queue    */
 #define MI_CLS_DLV_GROUPS 64
+/* Entries one delivery groups at most: a burst with more entries must give
+ * every entry qid 0xFF (mi_cls_deliver_submit rejects it otherwise). */
+#define MI_CLS_DLV_GROUP_MAX 8192
 
 typedef struct mi_cls_dlv_args {
 	const uint8_t *base;    /* the classified batch's base (host VA)           */
@@ -378,7 +381,8 @@ typedef struct mi_cls_dlv_args {
 /* Submit the delivery of a classified burst on the context's stream (after
  * its classification) and return a ticket for mi_cls_classify_host_wait.
  * Every pointer is host memory the device reads and writes in place
- * (mi_cls_host_alloc); entries with qid 0xFF are left out of perm. */
+ * (mi_cls_host_alloc); entries with qid 0xFF are left out of perm.  More
+ * than MI_CLS_DLV_GROUP_MAX entries with a queue group: -E2BIG. */
 int mi_cls_deliver_submit(mi_cls_ctx_t *ctx, const mi_cls_dlv_args_t *args, uint64_t *ticket);
 
 /* 1 if p lies in page-locked host memory that the device addresses at the

@@ -332,9 +332,9 @@ int odp_amd_cls_pktin_opt_set(odp_pktio_t pktio, uint64_t opt);
 void odp_amd_cls_queue_stats_add(uint32_t cos_index, uint32_t slot, uint64_t packets,
 				 uint64_t discards);
 
-/* 1 when every valid CoS has a pool of its own (no classified packet comes
- * from the pktio's pool), else 0. */
-int odp_amd_cls_all_cos_pooled(void);
+/* 1 when every valid CoS has a pool of its own other than pktio_pool (no
+ * classified packet comes from the pktio's pool), else 0. */
+int odp_amd_cls_all_cos_pooled(odp_pool_t pktio_pool);
 
 /* cos->pool of a CoS index (pool switch of the receive path). */
 odp_pool_t odp_amd_cls_pool_of(uint32_t cos_index);

@@ -1974,6 +1974,100 @@ __device__ __forceinline__ void bv_eval(const D &blk, T H, bool act, const Pkt &
 	hit = h ? 1u : hit;
 }
 
+// ---------------------------------------------------- tree-plan kernels
+// A program-specialised kernel for a CoS tree (tree programs whose levels are
+// joint groups, e.g. config 5: default CoS -> 16 VLAN CoS -> 128 prefix CoS
+// -> leaves) carries, besides the default CoS's block (round 1, DescC), the
+// tree's plan: S::nplan rounds, round i evaluating the lanes that sit on a
+// CoS of joint group S::gid[i] with that group's info words (S::ginfo[i], the
+// layout of the group info in the hot region) and class records
+// (S::grec[i][c]) compiled in -- no scalar loads and no decoding of group or
+// class words per tile.  Membership is tested per lane (the CoS entry's
+// group bits), so a lane is advanced only by the round of the group it sits
+// on: any lane off the plan (or deeper than it) stays pending and is finished
+// by the reference's scan (linear_scan) per CoS after the plan.  The host
+// builds a plan only when it covers every non-leaf destination of the tree.
+template <typename...> struct mi_void { typedef void type; };
+template <typename S, typename = void> struct plan_n {
+	static constexpr uint32_t v = 0;
+};
+template <typename S> struct plan_n<S, typename mi_void<decltype(S::nplan)>::type> {
+	static constexpr uint32_t v = S::nplan;
+};
+
+template <uint32_t V> struct mi_uconst {
+	static constexpr uint32_t value = V;
+};
+// f(mi_uconst<0>{}) .. f(mi_uconst<N - 1>{}), unrolled at compile time
+template <uint32_t N, uint32_t I = 0, typename F>
+__device__ __forceinline__ void static_for(F &f)
+{
+	if constexpr (I < N) {
+		f(mi_uconst<I>{});
+		static_for<N, I + 1>(f);
+	}
+}
+
+// One plan round's joint-group evaluation for the lanes in `bvl` (CoS slot
+// `cs`): the generic kernel's joint path (mi_cls_kernel) with the group's
+// words as compile-time constants.
+// (a plain function, not a lambda: clang's constant evaluator crashed on the
+// implicitly constexpr lambda's vector element stores)
+template <typename S, uint32_t I, uint32_t C>
+__device__ __forceinline__ DescV plan_rec()
+{
+	DescV d;
+#pragma unroll
+	for (uint32_t i = 0; i < 16; ++i)
+		d.v[i] = S::grec[I][C][i];
+	return d;
+}
+
+template <typename S, uint32_t I, typename T>
+__device__ __forceinline__ void plan_eval(T H, bool bvl, uint32_t cs, const Pkt &k, const Parsed &p,
+					  const Fields &x, uint32_t &hit, uint32_t &nxt, uint32_t &nmark,
+					  uint32_t &nleaf)
+{
+	constexpr const uint32_t *ji = S::ginfo[I];
+	uint32_t rw;
+	bool hv;
+	if constexpr (ji[0] == 0u) {
+		// direct: the first live rule's result word, or the CoS's miss word
+		const DescV cr = plan_rec<S, I, 0>();
+		uint32_t key[4], nk = cr(1);
+		const bool present = bv_key(cr, k, p, x, key);
+		joint_key(ji[14], cs, key, nk);
+		const uint32_t val = bv_probe(H, key, bvl && present, nk, ji[9], ji[10], ji[11], ji[12]);
+		const uint32_t miss = H[ji[13] + cs];
+		rw = val != 0u ? (val == BV_EMPTY ? 0u : val) : miss;
+		hv = rw != 0u;
+	} else {
+		// bitmap: AND of the classes' rule rows and the CoS's alive row
+		uint32_t acc = H[ji[2] + cs];
+		auto cls = [&](auto ic) {
+			constexpr uint32_t kc = decltype(ic)::value;
+			if constexpr (kc < ji[1]) {
+				constexpr const uint32_t *ci = ji + 8u + 8u * kc;
+				const DescV cr = plan_rec<S, I, kc>();
+				uint32_t key[4], nk = cr(1);
+				const bool present = bv_key(cr, k, p, x, key);
+				joint_key(ci[6], cs, key, nk);
+				const uint32_t val = bv_probe(H, key, bvl && present, nk, ci[1], ci[2], ci[3], ci[4]);
+				acc &= val != 0u ? val : H[ci[5] + cs];
+			}
+		};
+		static_for<BV_MAX_CLS>(cls);
+		const uint32_t res = H[ji[3] + cs];
+		rw = H[res + (acc != 0u ? (uint32_t)__builtin_ctz(acc) : 0u)];
+		hv = acc != 0u;
+	}
+	const bool h = bvl && hv;
+	nxt = h ? (rw & 0xffu) : nxt;
+	nleaf = h ? ((rw >> 8) & 1u) : nleaf;
+	nmark = h ? (rw >> 16) : nmark;
+	hit = h ? 1u : hit;
+}
+
 // Linear scan of one wave-uniform CoS's rule records for the lanes in
 // `grp` (verify_pmr over cos->pmr[] in order, first match wins).
 __device__ __forceinline__ void linear_scan(cword_t prog, uint32_t rec0, uint32_t nr, bool grp,
@@ -2360,7 +2454,13 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 
 		STAMP(0);   // data of this tile landed in LDS
 		// advance the pipeline: data of tile+stride, descriptors of tile+2*stride
+#ifdef DIAG_NOSTAGE
+		// diagnostic: every tile re-parses and re-classifies this wave's first
+		// tile (no window loads after it): the compute-only floor
+		if (false) {
+#else
 		if (PREFETCH) {
+#endif
 			d_off = n_off;
 			d_len = n_len;
 			const uint32_t t2 = tile + 2u * tstride, p2 = t2 * WAVE + lane;
@@ -2516,7 +2616,8 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 			if constexpr (!std::is_void<SPEC>::value) {
 				// the default CoS's block is compiled in (it has one: the
 				// host specialises only such programs)
-				bv_eval<FM>(DescC<SPEC>{ 0u, hc }, H, g, k, p, x, hit, nxt, nmark, nleaf);
+				bv_eval<FM>(DescC<SPEC>{ 0u, hc }, H, g, k, p, x, hit, nxt, nmark, nleaf,
+					    (uint32_t)max(def_cos, 0));
 			} else if constexpr (FM >= 0) {
 				bv_eval<FM>(DescU{ hc + d_bv, hc }, H, g, k, p, x, hit, nxt, nmark, nleaf);
 			} else {
@@ -2528,10 +2629,40 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 			}
 			advance(g ? 1u : 0u, hit, nxt, nmark, nleaf);
 		}
+		if constexpr (plan_n<SPEC>::v > 0) {
+			// tree-plan kernel: the plan's rounds, each for the lanes on its
+			// joint group, then the reference's scan for any lane still
+			// pending (off the plan)
+			auto round = [&](auto ic) {
+				constexpr uint32_t I = decltype(ic)::value;
+				if (__ballot(pend != 0u) == 0ull)
+					return;
+				const uint32_t cw = pend != 0u ? H[COS_WORDS * (uint32_t)cur + C_BV] : 0u;
+				const bool bvl = pend != 0u && ((cw >> 24) & 0x7fu) == SPEC::gid[I];
+				uint32_t hit = 0, nleaf = 0, nxt = 0, nmark = 0;
+				if (__ballot(bvl) != 0ull)
+					plan_eval<SPEC, I>(H, bvl, bvl ? (uint32_t)cur : 0u, k, p, x, hit, nxt, nmark,
+							   nleaf);
+				advance(bvl ? 1u : 0u, hit, nxt, nmark, nleaf);
+			};
+			static_for<plan_n<SPEC>::v>(round);
+			for (;;) {
+				const unsigned long long am = __ballot(pend != 0u);
+				if (am == 0ull)
+					break;
+				const int32_t c1 = __builtin_amdgcn_readlane(cur, (int)__builtin_ctzll(am));
+				const bool g = pend != 0u && cur == c1;
+				const cword_t ce = hc + COS_WORDS * (uint32_t)c1;
+				uint32_t hit = 0, nxt = 0, nmark = 0;
+				linear_scan(prog, ce[C_REC0], ce[C_NR], g, k, p, x, hit, nxt, nmark);
+				advance(g ? 1u : 0u, hit, nxt, nmark, 0u);
+			}
+		}
 #ifdef DIAG_MAXROUND
 		uint32_t diag_round = 1;
 #endif
-		for (; FM < 0;) {
+		// (the generic descent: not instantiated in tree-plan kernels)
+		if constexpr (plan_n<SPEC>::v == 0) for (; FM < 0;) {
 			const unsigned long long pm = __ballot(pend != 0u);
 			if (pm == 0ull)
 				break;

@@ -2,7 +2,7 @@
 //
 // After a burst is classified, the host decides each frame's fate (parse
 // drop, CoS drop / discard, destination pool), takes the packets, and hands
-// the device one 32-B mi_cls_dlv_t per delivered packet.  This kernel then
+// the device one 48-B mi_cls_dlv_t per delivered packet.  This kernel then
 // does the per-packet host steps of loopback_recv / pcapif_recv_pkt that
 // follow classification (platform/linux-generic/pktio/loop.c:308-373,
 // pcap.c:330-352) straight into page-locked host memory:
@@ -62,8 +62,9 @@ __device__ __forceinline__ void dlv_layer(uint32_t layer, uint32_t &fl, uint32_t
 // entry's place = its group's start + the entries of its group before it:
 // per 256-entry chunk a ballot loop over each wave's distinct qids gives the
 // rank inside the wave, the other waves' counts the rest.  Bursts of more
-// than DLV_GROUP_MAX entries are not grouped (the host leaves qid 0xFF).
-#define DLV_GROUP_MAX 8192
+// than DLV_GROUP_MAX entries are not grouped (the host leaves qid 0xFF;
+// mi_cls_deliver_submit checks it).
+#define DLV_GROUP_MAX MI_CLS_DLV_GROUP_MAX
 __device__ void dlv_group(const DArgs &a)
 {
 	__shared__ uint8_t s_q[DLV_GROUP_MAX];

@@ -1254,9 +1254,11 @@ int odp_amd_cls_cos_enq_mode(uint32_t cos_index, odp_pool_t *vec_pool, uint32_t 
 	return c->use_std_enq;
 }
 
-/* 1 when every valid CoS has a pool of its own: classified packets never
- * come from the pktio's pool (the receive path's pcap burst bound). */
-int odp_amd_cls_all_cos_pooled(void)
+/* 1 when every valid CoS has a pool of its own, other than the pktio's
+ * pool: classified packets never come from the pktio's pool (the receive
+ * path's pcap burst bound).  A CoS whose pool is the pktio's pool counts as
+ * unpooled. */
+int odp_amd_cls_all_cos_pooled(odp_pool_t pktio_pool)
 {
 	int all = 1, any = 0;
 
@@ -1265,7 +1267,7 @@ int odp_amd_cls_all_cos_pooled(void)
 		if (G.cos[i].valid && G.cos[i].action != ODP_COS_ACTION_DROP) {
 			/* (a drop CoS never takes a packet) */
 			any = 1;
-			if (G.cos[i].pool == ODP_POOL_INVALID)
+			if (G.cos[i].pool == ODP_POOL_INVALID || G.cos[i].pool == pktio_pool)
 				all = 0;
 		}
 	pthread_mutex_unlock(&G.lock);

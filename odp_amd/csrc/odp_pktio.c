@@ -112,6 +112,7 @@ typedef struct {
 	int pending;            /* staged (and submitted), not delivered */
 	uint64_t ticket;        /* odp_amd_cls_classify_host_submit, 0 = done */
 	uint64_t gen;           /* control-plane generation the set was submitted under */
+	uint64_t dgen;          /* generation its delivery was decided under (rx_dlv_start) */
 } rx_set_t;
 
 typedef struct {
@@ -159,6 +160,7 @@ static void rx_sets_free(rt_pktio_t *e);
 static void fbuf_free(rt_pktio_t *e);
 static int rx_finish(rt_pktio_t *e, rx_set_t *s, odp_packet_t out[], int max_out);
 static int rx_dlv_end(rt_pktio_t *e, rx_set_t *s, odp_packet_t out[], int max_out);
+static rx_set_t *rx_age(rt_pktio_t *e, int k);
 
 static rt_pktio_t PK[RT_MAX_PKTIO];
 static odp_spinlock_t pk_lock;
@@ -1842,6 +1844,7 @@ static int rx_dlv_start(rt_pktio_t *e, rx_set_t *s, rx_cnt_t *c)
 	    !mi_cls_host_mapped(s->base))
 		return -1;
 	const uint64_t td0 = prof_ns();
+	s->dgen = odp_amd_cls_generation();
 	/* per-burst caches of the CoS lookups (pool, queue of slot 0) */
 	odp_pool_t cpool[256];
 	odp_queue_t cq0[256];
@@ -2016,6 +2019,8 @@ static int rx_dlv_start(rt_pktio_t *e, rx_set_t *s, rx_cnt_t *c)
 	for (int k = 0; k < npl; k++)
 		if (pl[k].used < pl[k].have)
 			odp_packet_free_multi(&got[pl[k].base + pl[k].used], pl[k].have - pl[k].used);
+	if (ne > MI_CLS_DLV_GROUP_MAX)   /* larger than the device grouping serves */
+		grouped = 0;
 	if (!grouped)   /* per-run enqueue (vectors, aggregators, > 64 queues) */
 		for (uint32_t j = 0; j < ne; j++)
 			s->dlv[j].qid = 0xff;
@@ -2056,6 +2061,88 @@ static int rx_dlv_start(rt_pktio_t *e, rx_set_t *s, rx_cnt_t *c)
 	return 0;
 }
 
+/* The control plane changed while set s's GPU delivery was in flight: its
+ * packets' CoS, queues and pools were settled under the old tables, and a
+ * queue destroyed since may have had its slot reused by a new one.  The burst
+ * is classified again under the current tables and each delivered packet
+ * re-resolved from its new record -- what a receive call made after the
+ * change delivers: a packet whose outcome is no longer an enqueue is freed
+ * (CoS discards counted, and it leaves in_packets / in_octets), one whose CoS
+ * pool changed is copied into that pool, and every packet takes its CoS, mark
+ * and queue from the new record.  The burst is then enqueued per run. */
+static void rx_dlv_regen(rt_pktio_t *e, rx_set_t *s, rx_cnt_t *c)
+{
+	const odp_proto_layer_t layer = e->parse_layer;
+	uint32_t m = 0;
+	int rc = odp_amd_cls_classify_host(e->hdl, s->base, s->bytes, s->soff, s->slen, (uint32_t)s->n,
+					   s->res, 0);
+
+	s->grouped = 0;
+	if (rc) {
+		RT_ERR("pktio %s: GPU classify failed (%s), %u packets dropped\n", e->name,
+		       mi_cls_strerror(rc), s->ne);
+		odp_packet_free_multi(s->ent, (int)s->ne);
+		c->in_discards += s->ne;
+		s->ne = 0;
+		return;
+	}
+	for (uint32_t j = 0; j < s->ne; j++) {
+		odp_packet_t pkt = s->ent[j];
+		mi_cls_result_t r = s->res[s->dlv[j].rec];
+		const uint32_t len = s->dlv[j].len;
+
+		apply_layer(&r, layer);
+		if (r.outcome != MI_CLS_OUT_ENQ) {
+			if (r.outcome == MI_CLS_OUT_DISCARD || r.outcome == MI_CLS_OUT_LOOP)
+				c->in_discards++;
+			if (!r.err) {
+				c->packets--;
+				c->octets -= len;
+			}
+			odp_packet_free(pkt);
+			continue;
+		}
+		odp_pool_t pool = odp_amd_cls_pool_of(r.cos);
+
+		if (pool == ODP_POOL_INVALID)
+			pool = e->pool;
+		if (odp_packet_pool(pkt) != pool) {
+			/* _odp_pktio_packet_to_pool under the new CoS */
+			odp_packet_t np = odp_packet_alloc(pool, len);
+
+			if (np == ODP_PACKET_INVALID) {
+				c->in_discards++;
+				if (!r.err) {
+					c->packets--;
+					c->octets -= len;
+				}
+				odp_packet_free(pkt);
+				continue;
+			}
+			pkt_hdr_t *oh = rt_pkt_hdr(pkt), *nh = rt_pkt_hdr(np);
+
+			memcpy(odp_packet_data(np), oh->head + oh->data_off, len);
+			nh->in_flags = oh->in_flags;
+			nh->err = oh->err;
+			nh->l2 = oh->l2;
+			nh->l3 = oh->l3;
+			nh->l4 = oh->l4;
+			nh->input = oh->input;
+			nh->user_ptr = oh->user_ptr;
+			odp_packet_free(pkt);
+			pkt = np;
+		}
+		pkt_hdr_t *h = rt_pkt_hdr(pkt);
+
+		h->in_flags = r.in_flags;
+		h->cos = r.cos;
+		h->cls_mark = r.mark;
+		h->dst_queue = odp_amd_cls_queue_of(r.cos, r.queue);
+		s->ent[m++] = pkt;
+	}
+	s->ne = m;
+}
+
 /* End the GPU delivery of set s (rx_dlv_start): wait for the kernel, give
  * pool-switched packets their user pointers, enqueue (classifier on) or
  * return the packets in out[] (at most max_out), add the counters.
@@ -2090,6 +2177,8 @@ static int rx_dlv_end(rt_pktio_t *e, rx_set_t *s, odp_packet_t out[], int max_ou
 		odp_packet_free_multi(s->old, s->nold);
 		s->nold = 0;
 	}
+	if (e->cls_enabled && s->ne && s->dgen != odp_amd_cls_generation())
+		rx_dlv_regen(e, s, c);
 	const uint64_t tk1 = prof_ns();
 
 	if (!e->cls_enabled) {
@@ -2248,6 +2337,14 @@ static void rx_finish_start(rt_pktio_t *e, rx_set_t *s)
 		e->prof[2] += prof_ns() - t2;
 		return;
 	}
+	/* the host path delivers s now: every older burst still in its GPU
+	 * delivery is enqueued first, oldest first (arrival order per queue) */
+	for (int k = RX_SETS - 1; k > RX_CLS_DEPTH; k--) {
+		rx_set_t *b = rx_age(e, k);
+
+		if (b->delivering)
+			(void)rx_dlv_end(e, b, NULL, 0);
+	}
 	(void)rx_finish_host(e, s, &c, NULL, 0, t2);
 }
 
@@ -2296,7 +2393,7 @@ static int pktio_recv(rt_pktio_t *e, odp_packet_t out[], int max_out)
 		 * consumes the frame and stops on a failed allocation, pcap.c:324-327) */
 		/* (frames that all go to CoS with pools of their own never take a
 		 * packet of the pktio's pool: no bound then) */
-		if (rt_pool(e->pool) && !(e->cls_enabled && odp_amd_cls_all_cos_pooled())) {
+		if (rt_pool(e->pool) && !(e->cls_enabled && odp_amd_cls_all_cos_pooled(e->pool))) {
 			long room = (long)rt_pool_avail(e->pool) - pending_n;
 
 			if (room < (long)burst)

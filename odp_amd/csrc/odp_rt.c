@@ -516,6 +516,25 @@ static int pinned_pools(void)
 	return on;
 }
 
+/* ODP_AMD_PAGEABLE_POOLS=<name>[,<name>...]: packet pools of these names in
+ * ordinary memory (the others page-locked), so one receive burst can take
+ * the GPU delivery and the next the host's */
+static int pool_pageable(const char *name)
+{
+	const char *v = getenv("ODP_AMD_PAGEABLE_POOLS");
+	const size_t n = name ? strlen(name) : 0;
+
+	while (v && *v && n) {
+		const char *c = strchr(v, ',');
+		const size_t l = c ? (size_t)(c - v) : strlen(v);
+
+		if (l == n && strncmp(v, name, n) == 0)
+			return 1;
+		v = c ? c + 1 : NULL;
+	}
+	return 0;
+}
+
 int rt_pinned_arena(uint8_t **lo, size_t *bytes)
 {
 	uint8_t *a = NULL, *b = NULL;
@@ -608,7 +627,7 @@ odp_pool_t odp_pool_create(const char *name, const odp_pool_param_t *param)
 	 * addresses: the receive path then classifies loop packets in place and
 	 * the GPU writes received packets' metadata and frames into them
 	 * (ODP_AMD_PINNED_POOLS=0: ordinary memory, host delivery) */
-	if (param->type == ODP_POOL_PACKET && pinned_pools()) {
+	if (param->type == ODP_POOL_PACKET && pinned_pools() && !pool_pageable(name)) {
 		mem = mi_cls_host_alloc(esz * num);
 		if (mem && !mi_cls_host_mapped(mem)) {
 			mi_cls_host_free(mem);
@@ -763,6 +782,15 @@ static void pool_give(rt_pool_t *p, ev_hdr_t *const e[], int num)
 	if (num <= 0)
 		return;
 	odp_spinlock_lock(&p->lock);
+	if (p->num_free + (uint32_t)num > p->num) {
+		/* more events returned than the pool owns: a double free by the
+		 * application -- the excess is dropped, the free stack never grows
+		 * past the pool */
+		const uint32_t room = p->num - p->num_free;
+
+		RT_ERR("pool %s: %d events freed, room for %u (double free?)\n", p->name, num, room);
+		num = (int)room;
+	}
 	memcpy(p->free_stk + p->num_free, e, (size_t)num * sizeof(ev_hdr_t *));
 	p->num_free += (uint32_t)num;
 	odp_spinlock_unlock(&p->lock);

@@ -25,8 +25,9 @@
  * RX_COUNT_ONLY=1: no P lines; "R <packets delivered> <ns>" (receive-path
  *   rate, bench.py's runtime e2e: from odp_pktio_start to the last packet).
  * RX_SWITCH_RULES=<rules file> (direct mode): replayed after the first
- *   odp_pktin_recv call, while that call's burst is still in flight on the
- *   GPU (control-plane change between two receive calls).
+ *   odp_pktin_recv call (RX_SWITCH_AFTER=k: after the k-th), while earlier
+ *   bursts are still in flight on the GPU -- classification or delivery
+ *   (control-plane change between two receive calls).
  */
 #define _GNU_SOURCE
 #include <inttypes.h>
@@ -429,6 +430,7 @@ again:
 		if (odp_pktin_queue(pktio, &inq, 1) != 1)
 			return 11;
 		const char *sw = getenv("RX_SWITCH_RULES");
+		int sw_after = getenv("RX_SWITCH_AFTER") ? atoi(getenv("RX_SWITCH_AFTER")) : 1;
 
 		while (idle < 3) {
 			odp_time_t t0 = odp_time_local();
@@ -437,7 +439,7 @@ again:
 			odp_time_t t1 = odp_time_local();
 
 			recv_ns += odp_time_diff_ns(t1, t0);
-			if (sw) {
+			if (sw && --sw_after <= 0) {
 				FILE *f = fopen(sw, "r");
 
 				if (!f)

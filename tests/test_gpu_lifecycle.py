@@ -45,7 +45,8 @@ def _classify(prog, batch, spec_expected):
 def test_bench_order_replay(built, gpu):
     """bench.py's order in one process: a specialised main context kept
     alive, three flat programs specialised -> classified -> destroyed, then
-    config 5 at 1 M packets on the generic tree kernel.  Bit-exact."""
+    config 5 at 1 M packets on its tree-plan kernel and on the generic tree
+    kernel (MI_CLS_NO_PLAN).  Bit-exact."""
     from odp_amd.cls import Classifier
     mb, mp = R.config3(200_000)
     cm = Classifier(gpu=0)
@@ -62,12 +63,20 @@ def test_bench_order_replay(built, gpu):
             assert ll["specialised"] and not ll["div"], ll
             assert_same(got, oracle_run(p, b)[0], b, "flat extra")
         b5, p5 = R.config5(1_000_000)
-        got, ll = _classify(p5, b5, False)
-        assert ll["div"] and not ll["specialised"] and ll["flat_engine"] < 0, ll
         from oracle.oracle import Oracle
         o = Oracle()
         o.apply(p5)
-        assert_same(got, o.classify(b5, threads=16), b5, "config5 after specialised modules")
+        exp5 = o.classify(b5, threads=16)
+        got, ll = _classify(p5, b5, True)
+        assert ll["div"] and ll["specialised"] and ll["flat_engine"] < 0, ll
+        assert_same(got, exp5, b5, "config5 tree plan after specialised modules")
+        os.environ["MI_CLS_NO_PLAN"] = "1"
+        try:
+            got, ll = _classify(p5, b5, False)
+        finally:
+            del os.environ["MI_CLS_NO_PLAN"]
+        assert ll["div"] and not ll["specialised"] and ll["flat_engine"] < 0, ll
+        assert_same(got, exp5, b5, "config5 generic tree kernel after specialised modules")
     finally:
         cm.close()
 

@@ -161,9 +161,10 @@ def test_runtime_pktio_group_pipelined_rate(built, gpu, tmp_path):
     res = {}
     for gpus in ("0", "0,0,0"):
         res[gpus] = _rx_rate(pc, rules, {"ODP_AMD_GPUS": gpus})
-        # loops=5 replays the capture as the reference's pcap driver does
-        # (pcap.c:257-278: the count starts at 1)
-        assert res[gpus][1] == res["0"][1] >= 4 * b.n and res[gpus][2] == 0, res
+        # loops=5 replays the capture as the reference's pcap driver does:
+        # loop_cnt starts at 1 (pcap.c:214) and the driver stops when
+        # ++loop_cnt >= loops (pcap.c:265), so the capture passes 4 times
+        assert res[gpus][1] == res["0"][1] == 4 * b.n and res[gpus][2] == 0, res
     print("group pktio receive: " + ", ".join(f"{g}: {v[0]:.1f} Mpkt/s" for g, v in res.items()))
 
 

@@ -185,7 +185,7 @@ def _joint_tree(rng, n, leaf_kind):
     return b, prog
 
 
-@pytest.mark.parametrize("engine", ["auto", "nojoint", "wpb4", "linear"])
+@pytest.mark.parametrize("engine", ["auto", "nojoint", "wpb4", "linear", "spec", "nojit"])
 @pytest.mark.parametrize("leaf_kind", ["dport", "dip", "sip6"])
 def test_joint_direct_tree_levels(built, gpu, leaf_kind, engine):
     """A tree level whose CoS all key on one class is one joint direct group
@@ -258,7 +258,7 @@ def _joint_bitmap_tree(rng, n, pair):
     return b, prog
 
 
-@pytest.mark.parametrize("engine", ["auto", "nojoint", "wpb4", "linear"])
+@pytest.mark.parametrize("engine", ["auto", "nojoint", "wpb4", "linear", "spec", "nojit"])
 @pytest.mark.parametrize("pair", ["dport", "sip6"])
 def test_joint_bitmap_tree_levels(built, gpu, pair, engine):
     """A tree level whose CoS have bitmap blocks over the same two classes
@@ -387,7 +387,7 @@ def test_configs_full_size(built, gpu, cfg, kw, spec):
     """BASELINE configs at full size (1 M packets: one GPU's shard for
     configs 4 and 5): every record bit-exact vs the multithreaded oracle,
     with the generic kernels (MI_CLS_JIT=0) and with the program-specialised
-    kernel (waited for; config 5 is a tree and has none)."""
+    kernel (waited for; config 5's is its tree plan)."""
     import os
     from oracle.oracle import Oracle
     b, prog = (R.config3(1_000_000, **kw) if cfg == 3 else R.CONFIGS[cfg](1_000_000))

@@ -265,14 +265,18 @@ def test_rx_small_first_segment(built, gpu, tmp_path):
         assert len(got[0]["deep"]) == 1
 
 
-def test_rx_cos_destroyed_while_burst_in_flight(built, gpu, tmp_path):
-    """A hash-queue CoS is destroyed (and a new default CoS set) between two
-    odp_pktin_recv calls while the first call's burst is still in flight on
-    the GPU.  That burst was classified under the old rule snapshot; it must
-    be delivered under the current one (as the synchronous path would), not
-    to the destroyed CoS's queues: every packet the current rules enqueue
-    reaches the new CoS, and in_discards counts only the frames the oracle
-    discards (compare() checks the pktio counters)."""
+@pytest.mark.parametrize("switch_after", [1, 2, 3])
+def test_rx_cos_destroyed_while_burst_in_flight(built, gpu, tmp_path, switch_after):
+    """A hash-queue CoS is destroyed (its queues with it, and a new default
+    CoS with a new queue created) between two odp_pktin_recv calls while
+    earlier bursts are still in flight on the GPU: after call 1 the first
+    burst is being classified, after calls 2 and 3 the first bursts are in
+    their GPU delivery (queues and pools already settled under the old
+    tables).  Those bursts must be delivered under the current
+    tables (as the synchronous path would), not to the destroyed CoS's queues
+    or a queue that reused their slots: every packet the current rules
+    enqueue reaches the new CoS, and in_discards counts only the frames the
+    oracle discards (compare() checks the pktio counters)."""
     frames = H.pcap_frames([f for _, f in zoo.all_frames()])
     pc = str(tmp_path / "in.pcap")
     H.write_pcap(pc, frames)
@@ -285,7 +289,32 @@ def test_rx_cos_destroyed_while_burst_in_flight(built, gpu, tmp_path):
     # starts at 1, pcap.c:257-278) in bursts of 16: the first call's burst
     # stays in flight (more frames are waiting at the driver)
     got = H.run_driver(f"pcap:in={pc}:loops=3", r1, "direct", 4, 1, 1,
-                       env={"ODP_AMD_RX_BURST": "16", "RX_SWITCH_RULES": r2})
+                       env={"ODP_AMD_RX_BURST": "16", "RX_SWITCH_RULES": r2,
+                            "RX_SWITCH_AFTER": str(switch_after)})
     exp = H.expected(before + after, frames * 2, 1, 1, 4)
     H.compare(got, exp)
     assert got[0].get("B"), "nothing reached the new default CoS"
+
+
+def test_rx_mixed_delivery_paths_keep_order(built, gpu, tmp_path):
+    """Bursts that alternate between the GPU delivery and the host's (the
+    error CoS's pool is in ordinary memory, so a burst holding an error frame
+    is delivered on the host at once while older bursts may still be in their
+    GPU delivery): every queue still receives its packets in
+    arrival order, on pcap and loop pktios, as the reference's synchronous
+    receive does (pktio/loop.c:253-384)."""
+    frames = H.pcap_frames([f for _, f in zoo.all_frames()] * 3)
+    for pktio in ("pcap", "loop"):
+        _run_case(tmp_path, zoo.prog_everything(), frames, mode="direct", pktio=pktio,
+                  cos_pools=1, burst=8, env_extra={"ODP_AMD_PAGEABLE_POOLS": "errPool"})
+
+
+def test_rx_burst_above_device_grouping(built, gpu, tmp_path):
+    """Bursts larger than the delivery kernel's grouping serves
+    (MI_CLS_DLV_GROUP_MAX = 8192 entries): the burst is enqueued
+    per run instead, nothing is lost and every queue's order and counters are
+    the reference's."""
+    b, prog = R.config2(20000)
+    frames = [b.frame(i) for i in range(b.n)]
+    got = _run_case(tmp_path, prog, frames, mode="direct", burst=9000)
+    assert sum(len(v) for v in got[0].values()) == 20000

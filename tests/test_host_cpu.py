@@ -213,15 +213,19 @@ def test_classify_without_gpu_fails_loudly(c):
 
 
 @pytest.mark.parametrize("cfg,flat,spec", [(2, True, True), (3, True, True), (4, True, True),
-                                           ("nested1024", True, True), (5, False, False),
+                                           ("nested1024", True, True), (5, False, True),
+                                           ("5open", False, False),
                                            ("classes", False, True), ("noblock", False, False)])
 def test_specialised_kernel_compiles(built, cfg, flat, spec):
     """The embedded kernel sources compile with hipRTC (no GPU needed) into
     the program-specialised kernel of a flat program (every packet decided
-    on the default CoS's block in one round; candidate lists included) and
-    of a flat program whose default CoS has a chain of blocks (9 key
-    classes: no generic flat kernel, the chain compiled in); CoS trees
-    (config 5) and a default CoS without rules have none."""
+    on the default CoS's block in one round; candidate lists included), of a
+    flat program whose default CoS has a chain of blocks (9 key classes: no
+    generic flat kernel, the chain compiled in) and of a CoS tree whose
+    levels are joint groups (config 5: the tree plan compiled in).  A tree
+    whose plan does not cover it (config 5 plus a rule from a prefix CoS to
+    a CoS outside any joint group) and a default CoS without rules have
+    none."""
     L = cls.lib()
     L.mi_cls_spec_compile.restype = C.c_int
     L.mi_cls_spec_compile.argtypes = [C.c_void_p, C.c_size_t, C.c_int]
@@ -232,6 +236,14 @@ def test_specialised_kernel_compiles(built, cfg, flat, spec):
     elif cfg == "noblock":
         b, prog = R.config2(100)
         prog = [op for op in prog if op[0] != "pmr"]
+    elif cfg == "5open":
+        b, prog = R.config5(100)
+        ncos = sum(1 for op in prog if op[0] == "cos")
+        # a fourth level below one prefix CoS: "deep" has a rule of its own
+        # (to leaf 0) but is in no joint group, so the plan stops covering
+        prog = prog + [R.cos("deep", queue=900),
+                       ("pmr", [R.t_be16(R.PMR_UDP_SPORT, 7)], 17, ncos, 0),
+                       ("pmr", [R.t_u8(R.PMR_IPPROTO, 17)], ncos, 161, 0)]
     else:
         b, prog = R.CONFIGS[cfg](100)
     c = cls.Classifier(gpu=0)

@@ -129,3 +129,60 @@ def test_bench_world_size_mismatch_fails():
                         "--steps", "1", "--warmup", "0"], stdout=subprocess.PIPE,
                        stderr=subprocess.PIPE, text=True, timeout=120, env=env)
     assert r.returncode == 2 and "WORLD_SIZE=1" in r.stderr
+
+
+def _reduce_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    import bench
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    kw = bench.dist_init_kwargs("gloo", rank)
+    dist.init_process_group(rank=rank, world_size=world, **kw)
+    # rank r: wall 1 + r s, n = 1000 (r + 1) packets, kernel (r + 1) * 0.01 ms,
+    # bytes 1e6 (r + 1); rank 1 fails parity in the second call, in the
+    # third nobody checks
+    r1 = bench.reduce_ranks(dist, torch.device("cpu"), 1.0 + rank, 1000 * (rank + 1),
+                            0.01 * (rank + 1), 1_000_000 * (rank + 1), True)
+    r2 = bench.reduce_ranks(dist, torch.device("cpu"), 1.0, 10, 0.01, 1, rank != 1)
+    r3 = bench.reduce_ranks(dist, torch.device("cpu"), 1.0, 10, 0.01, 1, None)
+    q.put((rank, r1, r2["parity"], r3["parity"]))
+    dist.destroy_process_group()
+
+
+def test_bench_rank_reductions():
+    """bench.py's multi-rank reductions over gloo with 3 ranks: max wall,
+    packets summed, per-rank kernel_ms and bytes in rank order, the aggregate
+    roofline (sum of bytes / slowest kernel) and parity AND-ed over every
+    rank's shard (not rank 0's alone)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 3
+    ps = [ctx.Process(target=_reduce_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, r1, p2, p3 in res:
+        assert r1["wall"] == 3.0
+        assert r1["packets"] == 6000
+        assert r1["kernel_ms"] == [0.01, 0.02, 0.03]
+        assert r1["bytes_per_launch"] == [1_000_000, 2_000_000, 3_000_000]
+        assert abs(r1["achieved_gbs"] - 6e6 / 0.03e-3 / 1e9) < 1e-6
+        assert r1["parity"] is True and p2 is False and p3 is None
+
+
+def test_bench_nccl_init_binds_each_rank_to_its_device():
+    """The RCCL branch's init arguments for every local rank of an 8-GPU
+    node: device_id = cuda:LOCAL_RANK (the branch never runs on CPU; its
+    arguments are checked here)."""
+    import torch
+    import bench
+    for local in range(8):
+        kw = bench.dist_init_kwargs("nccl", local)
+        assert kw["backend"] == "nccl"
+        assert kw["device_id"] == torch.device(f"cuda:{local}")
+    assert bench.dist_init_kwargs("gloo", 3) == {"backend": "gloo"}
