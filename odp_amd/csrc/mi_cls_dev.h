@@ -964,7 +964,38 @@ static __constant__ L4Tab c_l4tab;
 // finish (IPv6 extension chain, L4 header past the window) set `slow` and are
 // re-parsed by parse_packet.  Results are identical to parse_packet for every
 // lane that does not set `slow`.
-__device__ __forceinline__ Parsed parse_fast(const Pkt &k, const uint32_t *l4tab, bool &slow)
+// The byte-dependent L4 header checks of parse_fast for one lane: TCP data
+// offset (l4+12; tcp = a TCP header that is not dropped), UDP length and,
+// for destination port 4500, the NAT-T marker (l4..l4+11; udp = a UDP header
+// that is not dropped).  Returns the error bits, the IPsec flag and `need`,
+// the bytes past l4 the checks read (the caller tests them against the
+// staged window).
+__device__ __forceinline__ void l4_bytes(const Pkt &k, uint32_t l4, bool tcp, bool udp, uint32_t &err,
+					 uint32_t &f, uint32_t &need)
+{
+	// L4 header bytes l4 .. l4+15 (dwords jl .. jl+4, byte shift 2)
+	const uint32_t jl = min((l4 - 2u) >> 2, (uint32_t)(WIN / 4 - 4));
+	uint32_t m[5], lb[4];
+#pragma unroll
+	for (int i = 0; i < 5; ++i)
+		m[i] = k.w[(jl + i) * RS];
+#pragma unroll
+	for (int i = 0; i < 4; ++i)
+		lb[i] = __builtin_amdgcn_alignbyte(m[i + 1], m[i], 2u);
+	const bool natt = (lb[0] >> 16) == 0x9411u;   // be16(4500) raw
+	need = tcp ? 13u : (udp ? (natt ? 12u : 6u) : 0u);
+	err = (tcp && ((lb[3] & 0xffu) >> 4) < 5u) ? E_TCP : 0u;
+	const uint32_t ulen = bsw16(lb[1]);
+	err |= (udp && ulen < 8u) ? E_UDP : 0u;
+	f = (udp && ulen >= 8u && natt && ulen > 4u && lb[2] != 0u) ? F_IPSEC : 0u;
+}
+
+// dwin != 0 (tree kernels): a lane longer than the staged window whose L4
+// check bytes lie in [k.win, dwin) is not sent to the general parser: `dfr`
+// is set, its L4 error bits and IPsec flag are left out, and the kernel
+// checks them (l4_bytes) once those bytes are staged.
+__device__ __forceinline__ Parsed parse_fast(const Pkt &k, const uint32_t *l4tab, bool &slow,
+					     uint32_t dwin, bool &dfr)
 {
 	Parsed r;
 	const uint32_t len = k.len;
@@ -1072,36 +1103,26 @@ __device__ __forceinline__ Parsed parse_fast(const Pkt &k, const uint32_t *l4tab
 	const uint32_t kc = pt >> 28;
 	const bool chk = kc != 0u && !non_first;   // a TCP / UDP / SCTP header to check
 	bool drop = false;
+	dfr = false;
 	if (__ballot(chk) != 0ull) {
-		// L4 header bytes l4 .. l4+15 (dwords jl .. jl+4, byte shift 2)
-		const uint32_t jl = min((l4 - 2u) >> 2, (uint32_t)(WIN / 4 - 4));
-		uint32_t m[5], lb[4];
-#pragma unroll
-		for (int i = 0; i < 5; ++i)
-			m[i] = k.w[(jl + i) * RS];
-#pragma unroll
-		for (int i = 0; i < 4; ++i)
-			lb[i] = __builtin_amdgcn_alignbyte(m[i + 1], m[i], 2u);
 		const bool tcp = chk && kc == L4K_TCP, udp = chk && kc == L4K_UDP;
 		const bool sctp = chk && kc == L4K_SCTP;
-		// bytes the checks below use: TCP data offset (l4+12), UDP ports and
-		// length (l4..l4+5) and, for destination port 4500, the NAT-T marker
-		// (l4+8..l4+11); a lane whose bytes are not all staged takes the
-		// general parser (the unused bytes of m[] may lie past the window)
-		const uint32_t l4need = tcp ? 13u : (udp ? (((lb[0] >> 16) == 0x9411u) ? 12u : 6u) : 0u);
-		sl = sl || (chk && l4 + l4need > k.win);
-		// TCP (parse_tcp, :299-316)
+		// TCP (parse_tcp, :299-316), UDP (parse_udp, :321-354), SCTP
+		// (parse_sctp, :362-388): the drops depend on the length only
 		const bool tcp_drop = tcp && l4 + 20u > len;
-		err |= (tcp && !tcp_drop && ((lb[3] & 0xffu) >> 4) < 5u) ? E_TCP : 0u;
-		// UDP (parse_udp, :321-354)
 		const bool udp_drop = udp && l4 + 8u > len;
-		const uint32_t ulen = bsw16(lb[1]);
-		const bool udp_ok = udp && !udp_drop;
-		err |= (udp_ok && ulen < 8u) ? E_UDP : 0u;
-		f |= (udp_ok && ulen >= 8u && (lb[0] >> 16) == 0x9411u && ulen > 4u && lb[2] != 0u)
-			? F_IPSEC : 0u;
-		// SCTP (parse_sctp, :362-388)
 		const bool sctp_drop = sctp && l4 + 12u > len;
+		uint32_t e4, f4, need;
+		l4_bytes(k, l4, tcp && !tcp_drop, udp && !udp_drop, e4, f4, need);
+		// a lane whose checked bytes are not all staged takes the general
+		// parser -- or, with a deferral window (dwin, tree kernels), has
+		// them checked once its bytes past the window are staged (l4_bytes
+		// again, mi_cls_kernel)
+		const bool far = chk && l4 + need > k.win;
+		dfr = far && l4 + need <= dwin && len > k.win;
+		sl = sl || (far && !dfr);
+		err |= dfr ? 0u : e4;
+		f |= dfr ? 0u : f4;
 		err |= (sctp && !sctp_drop && ((len - l4) & 0xffffu) < 12u) ? E_SCTP : 0u;
 		drop = tcp_drop || udp_drop || sctp_drop;
 	}
@@ -2392,6 +2413,16 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 #else
 	bool want_hi = a.hint == nullptr || *(const uint32_t *)a.hint + 1u == a.seq;
 #endif
+	// PLH (tree kernels without pktin options): bytes 64..WIN-1 are staged
+	// per lane, for the frames whose parse or program fields reach past byte
+	// 64 (a QinQ IPv6 frame's ports, an IPv6 TCP data offset), after the
+	// parse, instead of for every long frame of a tile the predictor marks:
+	// on config 5 those 96-B windows cost 1.33x the algorithmic HBM bytes.
+	// Their L4 checks (parse_fast: dfr) and the rounds after the first wait
+	// for them, so the first descent round runs while they are in flight.
+	constexpr bool PLH = DIV && !CK;
+	if constexpr (PLH)
+		want_hi = false;
 	bool saw_hi = false;
 	uint32_t d_win = WIN, my_win = WIN;
 	const uint32_t p_l3end = dev[DH_L3END], p_l4end = dev[DH_L4END], p_frend = dev[DH_FREND];
@@ -2454,29 +2485,37 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 
 		STAMP(0);   // data of this tile landed in LDS
 		// advance the pipeline: data of tile+stride, descriptors of tile+2*stride
+		// (PLH: after the parse, behind this tile's far loads in the vmcnt
+		// queue, so waiting for those never waits for the next tile's window)
+		auto prefetch = [&]() {
 #ifdef DIAG_NOSTAGE
-		// diagnostic: every tile re-parses and re-classifies this wave's first
-		// tile (no window loads after it): the compute-only floor
-		if (false) {
+			// diagnostic: every tile re-parses and re-classifies this wave's
+			// first tile (no window loads after it): the compute-only floor
+			if (false) {
 #else
-		if (PREFETCH) {
+			if (PREFETCH) {
 #endif
-			d_off = n_off;
-			d_len = n_len;
-			const uint32_t t2 = tile + 2u * tstride, p2 = t2 * WAVE + lane;
-			n_off = 0;
-			n_len = 0;
-			if (t2 < nt && p2 < a.n) {
-				n_off = ld_desc(a.off + p2);
-				n_len = ld_desc(a.len + p2);
+				d_off = n_off;
+				d_len = n_len;
+				const uint32_t t2 = tile + 2u * tstride, p2 = t2 * WAVE + lane;
+				n_off = 0;
+				n_len = 0;
+				if (t2 < nt && p2 < a.n) {
+					n_off = ld_desc(a.off + p2);
+					n_len = ld_desc(a.len + p2);
+				}
+				// no loads for a tile past the end (its registers would be
+				// waited for before reuse after the loop)
+				if (tile + tstride < nt)
+					d_hi = load_window(rs, d_off, d_len, lane, d, want_hi, d_win);
 			}
-			// no loads for a tile past the end (its registers would be
-			// waited for before reuse after the loop)
-			if (tile + tstride < nt)
-				d_hi = load_window(rs, d_off, d_len, lane, d, want_hi, d_win);
-		}
+		};
+		if constexpr (!PLH)
+			prefetch();
 		wave_lds_sync();
 #ifdef DIAG_STAGEONLY
+		if constexpr (PLH)
+			prefetch();
 		if (valid) {
 			uint4 rec;
 			rec.x = W[3 * RS + lane] ^ W[8 * RS + lane];
@@ -2492,13 +2531,14 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 		k.w = W + lane;
 		k.g = a.pkts + my_off;
 		k.len = my_len;
-		k.win = my_win;
+		k.win = PLH ? 64u : my_win;
 
 		STAMP(1);   // next tile's loads issued
 		Parsed p;
+		bool dfr = false;
 		if constexpr (!CK) {
 			bool slow;
-			p = parse_fast(k, s_l4, slow);
+			p = parse_fast(k, s_l4, slow, PLH ? (uint32_t)WIN : 0u, dfr);
 			if (__ballot(slow) != 0ull) {
 				if (slow)
 					p = parse_packet(k, 0u);
@@ -2511,7 +2551,7 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 			// A good IPv4 header checksum only adds l3_chksum_done.  Then
 			// the L4 checksums (whole frames from HBM, the wave cooperating).
 			bool slow;
-			p = parse_fast(k, s_l4, slow);
+			p = parse_fast(k, s_l4, slow, 0u, dfr);
 			p.udp_zero = 0;
 			slow = slow || p.err != 0u;
 			if (a.opt & OPT_IPV4_CK) {
@@ -2545,16 +2585,35 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 			if (a.opt & OPT_L4_CK)
 				l4_chksum(k, p, a.opt, rs, my_off, lane, valid, s_crc);
 		}
-		const Fields x = fields_of(k, p);
+		Fields x = fields_of(k, p);
+		// the bytes past byte 64 this lane uses: the parse's L3 / L4 headers
+		// and the program's fields (conservative: gates ignored)
+		uint32_t need;
 		{
-			// bytes this tile's lanes use: the parse's L3 / L4 headers and the
-			// program's fields (conservative: gates ignored)
-			// (reading a TCP data offset past a 64-B window from HBM instead
-			// of staging 96-B windows measured 3-6 % slower on configs 3-5)
 			const uint32_t l4h = (p.flags & F_TCP) ? 13u : ((p.flags & F_UDP) ? 6u : 0u);
-			uint32_t need = p_frend;
+			need = p_frend;
 			need = max(need, p.l3 != 0xFFFFu ? p.l3 + max(p_l3end, (p.flags & F_IPV6) ? 40u : 20u) : 0u);
 			need = max(need, p.l4 != 0xFFFFu ? p.l4 + max(p_l4end, l4h) : 0u);
+		}
+		u32x4 hv0 = { 0u, 0u, 0u, 0u }, hv1 = { 0u, 0u, 0u, 0u };
+		bool hneed = false, any_h = false;
+		if constexpr (PLH) {
+			// this tile's far pieces (bytes 64..95) for the lanes that need
+			// them, then the next tile's loads
+			hneed = valid && my_len > 64u && (need > 64u || dfr);
+			any_h = __ballot(hneed) != 0ull;
+			if (any_h) {
+				hv0 = __builtin_amdgcn_raw_buffer_load_b128(rs, hneed ? my_off + 64u : OOB_OFF, 0,
+									     LOAD_AUX);
+				hv1 = __builtin_amdgcn_raw_buffer_load_b128(
+					rs, hneed && my_len > 80u ? my_off + 80u : OOB_OFF, 0, LOAD_AUX);
+			}
+			prefetch();
+		} else {
+			// window predictor: the next tile stages bytes 64.. when this
+			// one's frames needed them
+			// (reading a TCP data offset past a 64-B window from HBM instead
+			// of staging 96-B windows measured 3-6 % slower on configs 3-5)
 #ifdef DIAG_FORCE_HI
 			want_hi = true;
 #else
@@ -2562,6 +2621,41 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 #endif
 			saw_hi = saw_hi || want_hi;
 		}
+		// PLH: the far pieces into the window (rows 16..), the lanes' windows
+		// widened, and the deferred L4 checks (parse_fast: dfr) on them
+		auto far_in = [&]() {
+			if constexpr (PLH) {
+				if (any_h) {
+					if (hneed) {
+#pragma unroll
+						for (uint32_t i = 0; i < 4; ++i) {
+							W[(16u + i) * RS + lane] = hv0[i];
+							W[(20u + i) * RS + lane] = hv1[i];
+						}
+						zero_tail(W, lane, my_len);
+					}
+					wave_lds_sync();
+					k.win = hneed ? (uint32_t)WIN : 64u;
+					x.k.win = k.win;
+					if (__ballot(dfr) != 0ull) {
+						uint32_t e4, f4, nd;
+						const bool tcp = dfr && (p.flags & F_TCP) != 0u && p.l4 + 20u <= my_len;
+						const bool udp = dfr && (p.flags & F_UDP) != 0u && p.l4 + 8u <= my_len;
+						l4_bytes(k, p.l4, tcp, udp, e4, f4, nd);
+						if (dfr) {
+							p.err |= e4;
+							p.flags |= f4;
+							p.ret = p.ret < 0 ? p.ret : (p.err != 0u ? 1 : 0);
+							x.f = p.flags;
+						}
+					}
+				}
+			}
+		};
+		// per-hop CoS counters count every hop a lane takes: no descent
+		// before the deferred checks then
+		if (stats_on)
+			far_in();
 #ifdef DIAG_PARSEONLY
 		if (valid) {
 			uint4 rec;
@@ -2578,8 +2672,8 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 		// Per-lane state is kept in integers updated by selects: bools live
 		// across the descent loop would become lane masks merged at every
 		// join (and spill SGPRs).
-		const bool ok_parse = valid && p.ret >= 0;
-		const bool perr = p.err != 0u;
+		bool ok_parse = valid && p.ret >= 0;
+		bool perr = p.err != 0u;
 		int32_t cur = perr ? err_cos : def_cos;
 		uint32_t pend = (ok_parse && !perr && def_cos >= 0 && def_valid) ? 1u : 0u;
 
@@ -2628,6 +2722,24 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 					linear_scan(prog, d_rec0, d_nr, g, k, p, x, hit, nxt, nmark);
 			}
 			advance(g ? 1u : 0u, hit, nxt, nmark, nleaf);
+		}
+		if constexpr (PLH) {
+			if (!stats_on) {
+				far_in();
+				// a deferred check found an L4 error: the lane goes to the
+				// error CoS (cls_select_cos) -- round 1 is undone
+				const bool nerr = p.err != 0u;
+				if (nerr && !perr) {
+					cur = err_cos;
+					pend = 0u;
+					hops = 0u;
+					mark = 0u;
+					matched = 0u;
+					loop = 0u;
+				}
+				perr = nerr;
+				ok_parse = valid && p.ret >= 0;
+			}
 		}
 		if constexpr (plan_n<SPEC>::v > 0) {
 			// tree-plan kernel: the plan's rounds, each for the lanes on its

@@ -536,3 +536,68 @@ def test_many_classes_in_tree(built, gpu, root_first, engine):
     assert info["tree"] and info["chained"] == 0
     got = both(tprog, b, what=f"classes9 tree root_first={root_first}", engine=engine)
     assert summary(got)["enq"] > 0
+
+
+def _far_l4_errors(n, stats):
+    """Config 5 traffic (VLAN / QinQ, IPv4 / IPv6, TCP / UDP) with L4 header
+    errors planted where their bytes lie past byte 64 -- IPv6 TCP data
+    offsets (byte 70 / 74) and QinQ IPv6 UDP lengths (bytes 66-67) -- and on
+    IPv4 frames, plus NAT-T destination ports (4500, marker at l4+8), under
+    config 5's tree with an error CoS (and per-CoS counters when `stats`)."""
+    from odp_amd import pktgen as pg
+    b, prog = R.config5(n)
+    rng = np.random.default_rng(505)
+    buf = b.buf
+    for i in range(b.n):
+        o = int(b.off[i])
+        f = bytes(buf[o:o + 64])
+        l3 = 14
+        while int.from_bytes(f[l3 - 2:l3], "big") in (0x8100, 0x88A8):
+            l3 += 4
+        et = int.from_bytes(f[l3 - 2:l3], "big")
+        l4 = l3 + (40 if et == 0x86DD else 20)
+        proto = f[l3 + 6] if et == 0x86DD else f[l3 + 9]
+        u = rng.random()
+        if proto == 6 and u < 0.08:
+            buf[o + l4 + 12] = 0x40                    # data offset 4 < 5: E_TCP
+        elif proto == 17 and u < 0.08:
+            buf[o + l4 + 4:o + l4 + 6] = [0, 4]        # UDP length 4 < 8: E_UDP
+        elif proto == 17 and u < 0.12:
+            buf[o + l4 + 2:o + l4 + 4] = [0x11, 0x94]  # dport 4500 (NAT-T marker test)
+    ncos = R.cos_count(prog)
+    prog = [(op[0], op[1], dict(op[2], stats=1 if stats and k % 3 == 0 else 0))
+            if op[0] == "cos" else op for k, op in enumerate(prog)]
+    prog.append(R.cos("l4err", queue=999, stats=1 if stats else 0))
+    prog.append(("error", ncos))
+    return b, prog
+
+
+@pytest.mark.parametrize("stats", [False, True], ids=["nostats", "stats"])
+@pytest.mark.parametrize("engine", ["spec", "nojit", "wpb4", "nojoint"])
+def test_far_l4_checks_deferred(built, gpu, engine, stats):
+    """Tree kernels stage bytes 64.. per lane after the parse and check the L4
+    headers whose bytes lie there once they land (the first descent round
+    runs meanwhile; a lane found in error is moved to the error CoS, as
+    cls_select_cos would have, odp_classification.c:1694-1726).  Records
+    bit-exact against the oracle, and with per-CoS counters (no deferral
+    then) the counters too (:1646-1647, 1721-1723)."""
+    from odp_amd.cls import Classifier
+    from oracle.oracle import Oracle
+    b, prog = _far_l4_errors(40_000, stats)
+    got = both(prog, b, what=f"far L4 errors stats={stats}", engine=engine)
+    s = summary(got)
+    assert s["enq"] > 0
+    assert np.count_nonzero(got["err"] & 0x18) > 500   # E_TCP / E_UDP found
+    if stats:
+        c = Classifier(gpu=0)
+        o = Oracle()
+        try:
+            cos, _ = c.apply(prog)
+            ocos, _ = o.apply(prog)
+            c.classify(b)
+            o.classify(b)
+            for h, oh in zip(cos, ocos):
+                if h:
+                    assert c.cos_stats_packets(h) == o.stats_packets(oh)
+        finally:
+            c.close()
