@@ -385,6 +385,89 @@ typedef struct mi_cls_dlv_args {
  * than MI_CLS_DLV_GROUP_MAX entries with a queue group: -E2BIG. */
 int mi_cls_deliver_submit(mi_cls_ctx_t *ctx, const mi_cls_dlv_args_t *args, uint64_t *ticket);
 
+/* ------------------------------------------------------------------------
+ * The receive chain: classification, the per-frame decisions and the
+ * delivery of one burst submitted at once, with no host step between them.
+ * The host's per-frame decide step of mi_cls_deliver_submit (parse drop,
+ * CoS drop / discard, destination pool, too long for the pool, queue group)
+ * runs on the device from a per-generation table of the control plane
+ * (mi_cls_rxtab_t: CoS -> pool slot, queues, queue groups), and each frame
+ * takes its packet from packets the host took from the pools before the
+ * submit (pool slot k: got[got_base[k] .. + have[k]), used in arrival order).
+ * A burst whose frames need more packets of a slot than were taken reports
+ * `short_pool` and is delivered again by the host (nothing it would deliver
+ * differently has been enqueued).  Reference steps: loop.c:308-373,
+ * pcap.c:330-352, include/odp_packet_io_internal.h:352-371,
+ * odp_classification.c:1742-1771, include/odp_classification_internal.h:
+ * 142-236.
+ * ---------------------------------------------------------------------- */
+#define MI_CLS_RX_POOLS 16
+#define MI_CLS_RX_QENT 1024
+#define MI_CLS_RXT_CLS   0x1u   /* classifier on                               */
+#define MI_CLS_RXT_GROUP 0x2u   /* every CoS enqueues plainly to <= 64 queues:   */
+				/* group by queue (qg) for one enqueue per queue */
+typedef struct mi_cls_rxtab {
+	uint32_t flags;               /* MI_CLS_RXT_*                               */
+	uint32_t npool;               /* pool slots (slot 0: the pktio's pool)      */
+	uint32_t pool_cap[MI_CLS_RX_POOLS];   /* data capacity of each slot's packets */
+	uint8_t  rt_slot[64];         /* runtime pool index -> slot + 1 (0: none)   */
+	uint8_t  cos_pool[256];       /* CoS index -> pool slot                     */
+	uint8_t  cos_nq[256];         /* queues of the CoS                          */
+	uint16_t cos_q0[256];         /* its first entry of qh / qg                 */
+	uint64_t qh[MI_CLS_RX_QENT];  /* odp_queue_t per (CoS, queue slot)          */
+	uint8_t  qg[MI_CLS_RX_QENT];  /* its queue group 0..63 (MI_CLS_RXT_GROUP)   */
+} mi_cls_rxtab_t;
+
+typedef struct mi_cls_rx_out {
+	uint64_t in_errors, in_discards, packets, octets;
+	uint32_t used[MI_CLS_RX_POOLS];   /* packets taken of each slot              */
+	uint32_t need[MI_CLS_RX_POOLS];   /* frames that wanted a packet of the slot */
+	uint32_t short_pool;          /* 1: a slot had too few packets (host redo)  */
+	uint32_t rsv[3];
+} mi_cls_rx_out_t;
+
+/* Frame decision word (dec[i]): fate in bits 0-1, pool slot in bits 2-6,
+ * queue group in bits 8-14 (0x7F none), rank among the slot's frames in
+ * bits 16-31. */
+#define MI_CLS_RXF_DROP    0u   /* parse drop or CoS drop: nothing delivered  */
+#define MI_CLS_RXF_DISCARD 1u   /* counted in in_discards                      */
+#define MI_CLS_RXF_FRESH   2u   /* a packet of its slot (frame copied)         */
+#define MI_CLS_RXF_INPLACE 3u   /* a loop packet received in its own buffer    */
+
+typedef struct mi_cls_rxc_args {
+	const uint8_t *base;          /* the burst's frames (soff[i] from here)     */
+	const uint32_t *soff;
+	const uint16_t *slen;
+	mi_cls_result_t *res;         /* records (written by the chain's classify)  */
+	uint32_t n;                   /* frames (<= MI_CLS_DLV_GROUP_MAX)           */
+	uint32_t layer;               /* parser layer (ODP_PROTO_LAYER_L2..ALL)     */
+	uint64_t input;               /* odp_pktio_t written into meta              */
+	uint32_t headroom;            /* data_off of fresh packets                  */
+	uint32_t data_from_meta;      /* bytes from a meta block to its data        */
+	const mi_cls_rxtab_t *tab;
+	const uint64_t *got;          /* packets taken per slot (odp_packet_t)      */
+	uint32_t got_base[MI_CLS_RX_POOLS], have[MI_CLS_RX_POOLS];
+	const uint64_t *pk;           /* loop: each frame's packet, else NULL       */
+	const uint8_t *ppool;         /* loop: its runtime pool index + 1           */
+	const uint16_t *pdoff;        /* loop: its headroom                         */
+	uint32_t meta_off;            /* bytes from a packet handle to its meta     */
+	uint32_t rsv;
+	/* outputs */
+	uint32_t *dec;                /* per frame: decision word                   */
+	uint64_t *ent;                /* per frame: the delivered packet (0: none)  */
+	uint32_t *perm;               /* frames grouped by queue group (stable)     */
+	uint32_t *gcnt;               /* MI_CLS_DLV_GROUPS counts                   */
+	mi_cls_rx_out_t *out;
+} mi_cls_rxc_args_t;
+
+/* Submit a host batch's classification (as mi_cls_classify_host_submit)
+ * followed by the decisions and the delivery of args; one ticket for all
+ * (mi_cls_classify_host_wait).  Every pointer of args is page-locked host
+ * memory the device addresses in place; res / soff / slen / base are the
+ * classification's.  -EINVAL: not so, or n too large. */
+int mi_cls_rx_chain_submit(mi_cls_ctx_t *ctx, const uint8_t *pkts, size_t bytes,
+			   const mi_cls_rxc_args_t *args, uint64_t *ticket);
+
 /* 1 if p lies in page-locked host memory that the device addresses at the
  * same address (the receive delivery's requirement), else 0. */
 int mi_cls_host_mapped(const void *p);

@@ -336,6 +336,20 @@ void odp_amd_cls_queue_stats_add(uint32_t cos_index, uint32_t slot, uint64_t pac
  * classified packet comes from the pktio's pool), else 0. */
 int odp_amd_cls_all_cos_pooled(odp_pool_t pktio_pool);
 
+/* The receive chain's per-generation table of the control plane for a
+ * pktio whose pool is pktio_pool (mi_cls_rxtab_t; pool_cap / rt_slot are the
+ * caller's); -1 when it does not fit. */
+struct mi_cls_rxtab;
+int odp_amd_cls_rxtab_fill(odp_pool_t pktio_pool, struct mi_cls_rxtab *tab, odp_pool_t pools[],
+			   uint32_t *npool, uint64_t *gen);
+
+/* One burst's receive chain: classification, decisions and delivery
+ * submitted at once on the pktio's GPU (mi_cls_rx_chain_submit); wait with
+ * odp_amd_cls_deliver_wait.  -ENOTSUP on pktios over several GPUs. */
+struct mi_cls_rxc_args;
+int odp_amd_cls_rx_chain(odp_pktio_t pktio, const uint8_t *pkts, size_t bytes,
+			 const struct mi_cls_rxc_args *args, uint64_t *ticket);
+
 /* cos->pool of a CoS index (pool switch of the receive path). */
 odp_pool_t odp_amd_cls_pool_of(uint32_t cos_index);
 

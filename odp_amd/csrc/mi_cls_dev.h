@@ -2962,6 +2962,11 @@ int mi_cls_launch_ck(int nw, bool lt, bool div, unsigned grid, size_t dyn, hipSt
 		     const KArgs &a);
 // receive delivery (mi_cls_kd.hip); grid 0: preload only
 int mi_cls_launch_deliver(unsigned grid, hipStream_t st, const mi_cls_dlv_args_t &h);
+// receive chain (mi_cls_kd.hip): decisions on `cls` after the burst's
+// classification, `dep` recorded there, the delivery on `dlv` after it;
+// preload: resolve both kernels only
+int mi_cls_launch_rx_chain(hipStream_t cls, hipStream_t dlv, hipEvent_t dep, const mi_cls_rxc_args_t &a,
+			   bool preload);
 
 // Every launcher goes through mi_launch.  grid == 0 launches nothing: it
 // resolves the instantiation on the current device (hipFuncGetAttributes

@@ -239,3 +239,277 @@ int mi_cls_launch_deliver(unsigned grid, hipStream_t st, const mi_cls_dlv_args_t
 	return hipLaunchKernel(reinterpret_cast<const void *>(&mi_cls_deliver_kernel), dim3(grid),
 			       dim3(DLV_THREADS), args, 0, st) == hipSuccess ? 0 : -EIO;
 }
+
+// ------------------------------------------------------------ receive chain
+// mi_cls_rx_chain_submit: after the burst's classification, on the device:
+// the per-frame decisions the host made for mi_cls_deliver_submit (one
+// block: mi_cls_rx_decide_kernel) and the delivery (mi_cls_rx_deliver_kernel).
+// The classifier is on, so the parser layer is ALL (odp_packet_io.c:
+// 675-677): records need no layer cut.
+#define RXD_THREADS 1024
+#define RXD_WAVES (RXD_THREADS / WAVE)
+
+// Decisions of frames [0, n) in arrival order: fate, pool slot, the frame's
+// rank among its slot's frames (the got packet it takes), queue group, and
+// the packet it is delivered in; the pktio counters; the stable grouping by
+// queue (as dlv_group); `short_pool` when a slot has too few packets.
+__global__ __launch_bounds__(RXD_THREADS) void mi_cls_rx_decide_kernel(mi_cls_rxc_args_t a)
+{
+	__shared__ uint8_t s_q[MI_CLS_DLV_GROUP_MAX];
+	__shared__ uint32_t s_w[RXD_WAVES][MI_CLS_RX_POOLS];   // per wave: fresh frames per slot
+	__shared__ uint32_t s_base[MI_CLS_RX_POOLS];           // frames of each slot so far
+	__shared__ uint32_t s_gw[RXD_WAVES][MI_CLS_DLV_GROUPS];
+	__shared__ uint32_t s_gcnt[MI_CLS_DLV_GROUPS], s_gpos[MI_CLS_DLV_GROUPS];
+	__shared__ unsigned long long s_ctr[4];
+	const uint32_t t = threadIdx.x, lane = t & (WAVE - 1), wave = t / WAVE;
+	const mi_cls_rxtab_t &tab = *a.tab;
+	const bool group = (tab.flags & MI_CLS_RXT_GROUP) != 0u;
+	const unsigned long long lt = lane ? (~0ull >> (64u - lane)) : 0ull;
+	if (t < MI_CLS_RX_POOLS)
+		s_base[t] = 0u;
+	if (t < MI_CLS_DLV_GROUPS)
+		s_gcnt[t] = 0u;
+	if (t < 4)
+		s_ctr[t] = 0ull;
+	__syncthreads();
+	unsigned long long errs = 0, disc = 0, pkts = 0, octs = 0;
+	for (uint32_t c0 = 0; c0 < a.n; c0 += RXD_THREADS) {
+		const uint32_t i = c0 + t;
+		const bool in = i < a.n;
+		mi_cls_result_t r = {};
+		if (in)
+			r = a.res[i];
+		const uint32_t len = in ? a.slen[i] : 0u;
+		uint32_t fate = MI_CLS_RXF_DROP, k = 0u;
+		if (in) {
+			errs += (r.err != 0u || r.outcome == MI_CLS_OUT_PARSE_DROP) ? 1u : 0u;
+			if (r.outcome == MI_CLS_OUT_DISCARD || r.outcome == MI_CLS_OUT_LOOP) {
+				fate = MI_CLS_RXF_DISCARD;
+			} else if (r.outcome == MI_CLS_OUT_ENQ) {
+				k = tab.cos_pool[r.cos];
+				const uint32_t own = a.pk && a.ppool[i] ? tab.rt_slot[a.ppool[i] - 1u] : 0u;
+				if (own != 0u && own - 1u == k)
+					fate = MI_CLS_RXF_INPLACE;
+				else if (len > tab.pool_cap[k])
+					fate = MI_CLS_RXF_DISCARD;   // odp_packet_alloc fails
+				else
+					fate = MI_CLS_RXF_FRESH;
+			}
+		}
+		// rank among the slot's fresh frames: the wave's lanes before this
+		// one (a ballot per slot present in the wave), then the earlier
+		// waves of the chunk and the earlier chunks
+		const bool fr = fate == MI_CLS_RXF_FRESH;
+		uint32_t rank = 0;
+		if (lane < MI_CLS_RX_POOLS)
+			s_w[wave][lane] = 0u;
+		{
+			bool left = fr;
+			for (;;) {
+				const unsigned long long m = __ballot(left);
+				if (!m)
+					break;
+				const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)k, (int)__builtin_ctzll(m));
+				const unsigned long long mv = __ballot(left && k == v);
+				if (left && k == v) {
+					rank = (uint32_t)__popcll(mv & lt);
+					left = false;
+				}
+				if (lane == 0)
+					s_w[wave][v] = (uint32_t)__popcll(mv);
+			}
+		}
+		__syncthreads();
+		if (fr) {
+			for (uint32_t w = 0; w < wave; ++w)
+				rank += s_w[w][k];
+			rank += s_base[k];
+		}
+		const bool got = fr && rank < a.have[k];
+		const bool dlv = got || fate == MI_CLS_RXF_INPLACE;
+		if (fate == MI_CLS_RXF_DISCARD)
+			++disc;
+		if (dlv && r.err == 0u) {
+			++pkts;
+			octs += len;
+		}
+		const uint32_t qe = in && r.outcome == MI_CLS_OUT_ENQ ? tab.cos_q0[r.cos] + r.queue : 0u;
+		const uint32_t qid = dlv && group ? tab.qg[qe] : 0x7Fu;
+		if (in) {
+			a.dec[i] = fate | (k << 2) | ((qid & 0x7Fu) << 8) | (min(rank, 0xFFFFu) << 16);
+			a.ent[i] = got ? a.got[a.got_base[k] + rank] : (fate == MI_CLS_RXF_INPLACE ? a.pk[i] : 0ull);
+			s_q[i] = (uint8_t)(qid < MI_CLS_DLV_GROUPS ? qid : 0xFFu);
+		}
+		__syncthreads();
+		if (t < MI_CLS_RX_POOLS) {
+			uint32_t all = 0;
+			for (uint32_t w = 0; w < RXD_WAVES; ++w)
+				all += s_w[w][t];
+			s_base[t] += all;
+		}
+		__syncthreads();
+	}
+	// counters (a slot short of packets shows in s_base > have below)
+	if (errs)
+		atomicAdd(&s_ctr[0], errs);
+	if (disc)
+		atomicAdd(&s_ctr[1], disc);
+	if (pkts)
+		atomicAdd(&s_ctr[2], pkts);
+	if (octs)
+		atomicAdd(&s_ctr[3], octs);
+	__syncthreads();
+	if (t == 0) {
+		a.out->in_errors = s_ctr[0];
+		a.out->in_discards = s_ctr[1];
+		a.out->packets = s_ctr[2];
+		a.out->octets = s_ctr[3];
+		uint32_t sh = 0;
+		for (uint32_t k = 0; k < MI_CLS_RX_POOLS; ++k) {
+			a.out->used[k] = min(s_base[k], a.have[k]);
+			a.out->need[k] = s_base[k];
+			sh |= s_base[k] > a.have[k] ? 1u : 0u;
+		}
+		a.out->short_pool = sh;
+	}
+	if (!group)
+		return;
+	// the stable permutation of the delivered frames by queue group
+	for (uint32_t i = t; i < a.n; i += RXD_THREADS)
+		if (s_q[i] < MI_CLS_DLV_GROUPS)
+			atomicAdd(&s_gcnt[s_q[i]], 1u);
+	__syncthreads();
+	if (t == 0) {
+		uint32_t at = 0;
+		for (uint32_t g = 0; g < MI_CLS_DLV_GROUPS; ++g) {
+			s_gpos[g] = at;
+			at += s_gcnt[g];
+		}
+	}
+	if (t < MI_CLS_DLV_GROUPS)
+		a.gcnt[t] = s_gcnt[t];
+	__syncthreads();
+	for (uint32_t c0 = 0; c0 < a.n; c0 += RXD_THREADS) {
+		const uint32_t i = c0 + t;
+		const uint32_t q = i < a.n ? s_q[i] : 0xFFu;
+		bool left = q < MI_CLS_DLV_GROUPS;
+		uint32_t rank = 0;
+		if (lane < MI_CLS_DLV_GROUPS)
+			s_gw[wave][lane] = 0u;
+		for (;;) {
+			const unsigned long long m = __ballot(left);
+			if (!m)
+				break;
+			const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)q, (int)__builtin_ctzll(m));
+			const unsigned long long mv = __ballot(left && q == v);
+			if (left && q == v) {
+				rank = (uint32_t)__popcll(mv & lt);
+				left = false;
+			}
+			if (lane == 0)
+				s_gw[wave][v] = (uint32_t)__popcll(mv);
+		}
+		__syncthreads();
+		if (q < MI_CLS_DLV_GROUPS) {
+			uint32_t before = 0;
+			for (uint32_t w = 0; w < wave; ++w)
+				before += s_gw[w][q];
+			a.perm[s_gpos[q] + before + rank] = i;
+		}
+		__syncthreads();
+		if (t < MI_CLS_DLV_GROUPS) {
+			uint32_t all = 0;
+			for (uint32_t w = 0; w < RXD_WAVES; ++w)
+				all += s_gw[w][t];
+			s_gpos[t] += all;
+		}
+		__syncthreads();
+	}
+}
+
+// The delivery of the decided frames: 16 frames per block, 16 lanes each
+// (lanes 0-3: the 64-B metadata line, all 16: the frame copy), as
+// mi_cls_deliver_kernel.  A fresh packet gets the whole line; a loop packet
+// received in its own buffer keeps its headroom and user pointer (read from
+// its line), and a pool switch takes the old packet's user pointer.
+__global__ __launch_bounds__(DLV_THREADS) void mi_cls_rx_deliver_kernel(mi_cls_rxc_args_t a)
+{
+	const uint32_t sub = threadIdx.x & 15u;
+	const uint32_t i = blockIdx.x * DLV_PER_BLOCK + (threadIdx.x >> 4);
+	if (i >= a.n)
+		return;
+	const uint64_t e = a.ent[i];
+	if (!e)
+		return;
+	const uint32_t fate = a.dec[i] & 3u;
+	const bool fresh = fate == MI_CLS_RXF_FRESH;
+	uint8_t *meta = (uint8_t *)(uintptr_t)(e + a.meta_off);
+	const uint32_t len = a.slen[i];
+	if (sub < 4u) {
+		const mi_cls_result_t r = a.res[i];
+		const mi_cls_rxtab_t &tab = *a.tab;
+		const uint64_t dq = tab.qh[tab.cos_q0[r.cos] + r.queue];
+		u32x4 v;
+		if (sub == 0u) {
+			const uint32_t doff = fresh ? a.headroom : ((const u32x4 *)meta)[0][0];
+			v = u32x4{ doff, len, r.in_flags, 0u };
+		} else if (sub == 1u) {
+			v = u32x4{ (uint32_t)r.err | ((uint32_t)r.cos << 8) | ((uint32_t)r.mark << 16),
+				   (uint32_t)r.l3_offset << 16, r.l4_offset, 0u };
+		} else if (sub == 2u) {
+			v = u32x4{ (uint32_t)dq, (uint32_t)(dq >> 32), (uint32_t)a.input,
+				   (uint32_t)(a.input >> 32) };
+		} else {
+			// user pointer: kept in place; a pool switch takes the old
+			// packet's; a pcap frame has none
+			uint64_t up = 0u;
+			if (!fresh)
+				up = ((const mi_cls_pkt_meta_t *)meta)->user_ptr;
+			else if (a.pk)
+				up = ((const mi_cls_pkt_meta_t *)(uintptr_t)(a.pk[i] + a.meta_off))->user_ptr;
+			v = u32x4{ (uint32_t)up, (uint32_t)(up >> 32), 0u, 0u };
+		}
+		((u32x4 *)meta)[sub] = v;
+	}
+	if (fresh) {
+		const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+			(void *)a.base, (short)0, (int)OOB_OFF, 0x00020000);
+		const uint32_t src = a.soff[i];
+		u32x4 *dst = (u32x4 *)(meta + a.data_from_meta);
+		for (uint32_t o0 = 16u * sub; o0 < len; o0 += 6u * 256u) {
+			u32x4 v[6];
+#pragma unroll
+			for (uint32_t k = 0; k < 6; ++k) {
+				const uint32_t o = o0 + 256u * k;
+				v[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, o < len ? src + o : OOB_OFF, 0, 0);
+			}
+#pragma unroll
+			for (uint32_t k = 0; k < 6; ++k) {
+				const uint32_t o = o0 + 256u * k;
+				if (o < len)
+					dst[o >> 4] = v[k];
+			}
+		}
+	}
+}
+
+int mi_cls_launch_rx_chain(hipStream_t cls, hipStream_t dlv, hipEvent_t dep, const mi_cls_rxc_args_t &a,
+			   bool preload)
+{
+	if (preload) {
+		hipFuncAttributes fa;
+		return hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(&mi_cls_rx_decide_kernel)) ==
+				       hipSuccess &&
+			       hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(&mi_cls_rx_deliver_kernel)) ==
+				       hipSuccess ? 0 : -EIO;
+	}
+	mi_cls_rxc_args_t h = a;
+	void *args[] = { &h };
+	if (hipLaunchKernel(reinterpret_cast<const void *>(&mi_cls_rx_decide_kernel), dim3(1),
+			    dim3(RXD_THREADS), args, 0, cls) != hipSuccess ||
+	    hipEventRecord(dep, cls) != hipSuccess || hipStreamWaitEvent(dlv, dep, 0) != hipSuccess)
+		return -EIO;
+	const unsigned grid = (a.n + DLV_PER_BLOCK - 1u) / DLV_PER_BLOCK;
+	return hipLaunchKernel(reinterpret_cast<const void *>(&mi_cls_rx_deliver_kernel), dim3(grid),
+			       dim3(DLV_THREADS), args, 0, dlv) == hipSuccess ? 0 : -EIO;
+}

@@ -1274,6 +1274,102 @@ int odp_amd_cls_all_cos_pooled(odp_pool_t pktio_pool)
 	return any && all;
 }
 
+/* The receive chain's table (mi_cls_rxtab_t, mi_cls.h) for a pktio whose
+ * own pool is pktio_pool: per CoS index its pool slot (slot 0: the pktio's
+ * pool; a CoS without a pool of its own takes it, _odp_cls_classify_packet
+ * :1760-1764), its queues (get_dest_queue, :395-405) and their queue groups
+ * (every enqueueing CoS with the plain enqueue -- no packet vectors, no
+ * aggregators -- and at most 64 queues in all: one group per queue).
+ * pools[] / *npool: each slot's pool; *gen: the generation the table
+ * reflects.  The caller fills pool_cap / rt_slot (runtime pools).  -1 when
+ * the control plane does not fit the table. */
+int odp_amd_cls_rxtab_fill(odp_pool_t pktio_pool, struct mi_cls_rxtab *tab, odp_pool_t pools[],
+			   uint32_t *npool, uint64_t *gen)
+{
+	odp_queue_t gq[MI_CLS_DLV_GROUPS];
+	uint32_t np = 1, nq = 0, ng = 0;
+	int plain = 1, rc = 0;
+
+	memset(tab, 0, sizeof(*tab));
+	pools[0] = pktio_pool;
+	pthread_mutex_lock(&G.lock);
+	*gen = G.gen;
+	for (uint32_t i = 0; G.init && i < G.max_cos && i < 256 && rc == 0; i++) {
+		const cos_t *c = &G.cos[i];
+
+		if (!c->valid)
+			continue;
+		const odp_pool_t pool = c->pool != ODP_POOL_INVALID ? c->pool : pktio_pool;
+		uint32_t k = 0;
+
+		while (k < np && pools[k] != pool)
+			k++;
+		if (k == np) {
+			if (np == MI_CLS_RX_POOLS) {
+				rc = -1;
+				break;
+			}
+			pools[np++] = pool;
+		}
+		const uint32_t n = c->queue_group ? c->num_queue : 1u;
+
+		if (nq + n > MI_CLS_RX_QENT) {
+			rc = -1;
+			break;
+		}
+		tab->cos_pool[i] = (uint8_t)k;
+		tab->cos_nq[i] = (uint8_t)n;
+		tab->cos_q0[i] = (uint16_t)nq;
+		for (uint32_t j = 0; j < n; j++) {
+			const odp_queue_t q = c->queue_group ? c->hq[j] : c->queue;
+			uint32_t g = 0;
+
+			while (g < ng && gq[g] != q)
+				g++;
+			if (g == ng && c->action == ODP_COS_ACTION_ENQUEUE) {
+				if (ng == MI_CLS_DLV_GROUPS)
+					plain = 0;
+				else
+					gq[ng++] = q;
+			}
+			tab->qh[nq + j] = (uint64_t)(uintptr_t)q;
+			tab->qg[nq + j] = (uint8_t)(g < ng ? g : 0xFFu);
+		}
+		nq += n;
+		if (c->action == ODP_COS_ACTION_ENQUEUE && (c->use_std_enq <= 0 || c->use_aggr))
+			plain = 0;
+	}
+	pthread_mutex_unlock(&G.lock);
+	tab->flags = MI_CLS_RXT_CLS | (plain ? MI_CLS_RXT_GROUP : 0u);
+	tab->npool = np;
+	*npool = np;
+	return rc;
+}
+
+/* One burst's receive chain (mi_cls_rx_chain_submit) on the pktio's
+ * context, under the current rules.  -ENOTSUP for pktios over several
+ * devices (they take the host-decided delivery). */
+int odp_amd_cls_rx_chain(odp_pktio_t h, const uint8_t *pkts, size_t bytes,
+			 const struct mi_cls_rxc_args *args, uint64_t *ticket)
+{
+	pktio_t *e = get_pktio(h);
+	int rc;
+
+	if (!e || !ticket)
+		return -EINVAL;
+	*ticket = 0;
+	if (e->grp)
+		return -ENOTSUP;
+	rc = ensure_ctx(e);
+	if (rc)
+		return rc;
+	rc = sync_rules(e, NULL);
+	if (rc)
+		return rc;
+	mi_cls_pktin_opt_set(e->ctx, e->pktin_opt);
+	return mi_cls_rx_chain_submit(e->ctx, pkts, bytes, args, ticket);
+}
+
 /* cos->pool of the final CoS (_odp_cls_classify_packet, :1760-1764) */
 odp_pool_t odp_amd_cls_pool_of(uint32_t cos_index)
 {

@@ -113,6 +113,18 @@ typedef struct {
 	uint64_t ticket;        /* odp_amd_cls_classify_host_submit, 0 = done */
 	uint64_t gen;           /* control-plane generation the set was submitted under */
 	uint64_t dgen;          /* generation its delivery was decided under (rx_dlv_start) */
+	/* receive chain (rxc_submit .. rxc_end): the burst classified, decided
+	 * and delivered by the GPU from one submission, `delivering` from it */
+	int chain;
+	int pk_pinned;          /* pk / ppool page-locked */
+	int rxc_pinned;         /* dec / cent / got / rxo page-locked */
+	uint32_t *dec;          /* per frame: decision word (MI_CLS_RXF_*, mi_cls.h) */
+	uint64_t *cent;         /* per frame: its packet, 0 none */
+	uint64_t *got;          /* packets taken for the burst, per pool slot */
+	uint32_t got_cap;
+	mi_cls_rx_out_t *rxo;
+	uint32_t cnp, cbase[MI_CLS_RX_POOLS], chave[MI_CLS_RX_POOLS];
+	odp_pool_t cpool[MI_CLS_RX_POOLS];
 } rx_set_t;
 
 typedef struct {
@@ -149,6 +161,13 @@ typedef struct {
 	 * previous one is delivered (pipelined receive) */
 	rx_set_t rs[RX_SETS];
 	int cur;                /* set the next burst is staged into */
+	/* receive chain: the control plane's table (per generation), the pools
+	 * of its slots and how many packets of each a burst is given */
+	mi_cls_rxtab_t *rxtab;
+	int rxtab_pinned, rxtab_ok;
+	uint64_t rxtab_gen;
+	odp_pool_t rx_pools[MI_CLS_RX_POOLS];
+	uint32_t rx_np, rx_want[MI_CLS_RX_POOLS];
 	uint64_t prof[14];      /* ODP_AMD_RX_PROF: ns staging / classifying / delivering, bursts,
 				 * then of delivering: ns preparing / enqueueing, TSC ticks in
 				 * packet allocation / frame copies; GPU delivery: ns deciding +
@@ -161,6 +180,7 @@ static void fbuf_free(rt_pktio_t *e);
 static int rx_finish(rt_pktio_t *e, rx_set_t *s, odp_packet_t out[], int max_out);
 static int rx_dlv_end(rt_pktio_t *e, rx_set_t *s, odp_packet_t out[], int max_out);
 static rx_set_t *rx_age(rt_pktio_t *e, int k);
+static int stage_reserve(rx_set_t *s, uint32_t n, size_t bytes);
 
 static rt_pktio_t PK[RT_MAX_PKTIO];
 static odp_spinlock_t pk_lock;
@@ -773,6 +793,10 @@ int odp_pktio_start(odp_pktio_t h)
 			       mi_cls_strerror(rc));
 			return -1;
 		}
+		/* the burst sets' page-locked arrays too: made here, not by the
+		 * first bursts (each page-locked allocation is a runtime call) */
+		for (int k = 0; k < RX_SETS; k++)
+			(void)stage_reserve(&e->rs[k], rx_burst(), 0);
 	}
 	e->state = ST_STARTED;
 	if (e->param.in_mode == ODP_PKTIN_MODE_SCHED) {
@@ -901,7 +925,7 @@ static void rx_set_arrays_free(rx_set_t *s)
 	hmem_free(s->gcnt, s->dlv_pinned);
 	free(s->ent);
 	free(s->old);
-	free(s->ppool);
+	hmem_free(s->ppool, s->pk_pinned);
 	free(s->pdoff);
 	free(s->pup);
 	s->pup = NULL;
@@ -913,7 +937,17 @@ static void rx_set_arrays_free(rx_set_t *s)
 	s->ppool = NULL;
 	s->pdoff = NULL;
 	s->dlv_pinned = 0;
-	free(s->pk);
+	hmem_free(s->pk, s->pk_pinned);
+	hmem_free(s->dec, s->rxc_pinned);
+	hmem_free(s->cent, s->rxc_pinned);
+	hmem_free(s->got, s->rxc_pinned);
+	hmem_free(s->rxo, s->rxc_pinned);
+	s->dec = NULL;
+	s->cent = NULL;
+	s->got = NULL;
+	s->rxo = NULL;
+	s->got_cap = 0;
+	s->rxc_pinned = 0;
 	free(s->tmp);
 	s->tmp = NULL;
 	s->tmp_cap = 0;
@@ -926,6 +960,12 @@ static void rx_set_arrays_free(rx_set_t *s)
 
 static void rx_sets_free(rt_pktio_t *e)
 {
+	hmem_free(e->rxtab, e->rxtab_pinned);
+	e->rxtab = NULL;
+	e->rxtab_pinned = 0;
+	e->rxtab_ok = 0;
+	e->rxtab_gen = 0;
+	e->rx_np = 0;
 	for (int k = 0; k < RX_SETS; k++) {
 		rx_set_t *s = &e->rs[k];
 
@@ -947,7 +987,17 @@ static int stage_reserve(rx_set_t *s, uint32_t n, size_t bytes)
 		s->slen = hmem_alloc(c * sizeof(uint16_t), &p2);
 		s->res = hmem_alloc(c * sizeof(mi_cls_result_t), &p3);
 		s->arr_pinned = p1;
-		s->pk = malloc(c * sizeof(odp_packet_t));
+		int k1, k2;
+
+		s->pk = hmem_alloc(c * sizeof(odp_packet_t), &k1);
+		s->ppool = hmem_alloc(c, &k2);
+		s->pk_pinned = k1 && k2;
+		if (k1 != k2 && s->pk && s->ppool) {   /* mixed: ordinary copies */
+			hmem_free(s->pk, k1);
+			hmem_free(s->ppool, k2);
+			s->pk = malloc(c * sizeof(odp_packet_t));
+			s->ppool = malloc(c);
+		}
 		if (p1 != p2 || p1 != p3) {   /* mixed: keep the pageable copies */
 			hmem_free(s->soff, p1);
 			hmem_free(s->slen, p2);
@@ -969,12 +1019,33 @@ static int stage_reserve(rx_set_t *s, uint32_t n, size_t bytes)
 		s->gcnt = hmem_alloc(MI_CLS_DLV_GROUPS * sizeof(uint32_t), &q3);
 		s->ent = malloc(c * sizeof(odp_packet_t));
 		s->old = malloc(c * sizeof(odp_packet_t));
-		s->ppool = malloc(c);
 		s->pdoff = malloc(c * sizeof(uint16_t));
 		s->pup = malloc(c * sizeof(void *));
 		if (!s->ppool || !s->pdoff || !s->pup) {
 			rx_set_arrays_free(s);
 			return -1;
+		}
+		/* receive chain arrays (page-locked or none) */
+		{
+			int r1, r2, r3, r4;
+
+			s->dec = hmem_alloc(c * sizeof(uint32_t), &r1);
+			s->cent = hmem_alloc(c * sizeof(uint64_t), &r2);
+			s->got = hmem_alloc((size_t)4 * c * sizeof(uint64_t), &r3);
+			s->rxo = hmem_alloc(sizeof(mi_cls_rx_out_t), &r4);
+			s->rxc_pinned = r1 && r2 && r3 && r4;
+			s->got_cap = 4u * c;
+			if (!s->rxc_pinned) {
+				hmem_free(s->dec, r1);
+				hmem_free(s->cent, r2);
+				hmem_free(s->got, r3);
+				hmem_free(s->rxo, r4);
+				s->dec = NULL;
+				s->cent = NULL;
+				s->got = NULL;
+				s->rxo = NULL;
+				s->got_cap = 0;
+			}
 		}
 		s->dlv_pinned = q1 && q2 && q3 && s->dlv && s->perm && s->gcnt && s->ent && s->old;
 		if (!s->dlv_pinned) {
@@ -2147,8 +2218,12 @@ static void rx_dlv_regen(rt_pktio_t *e, rx_set_t *s, rx_cnt_t *c)
  * pool-switched packets their user pointers, enqueue (classifier on) or
  * return the packets in out[] (at most max_out), add the counters.
  * Returns the packets placed in out[]. */
+static int rxc_end(rt_pktio_t *e, rx_set_t *s, odp_packet_t out[], int max_out);
+
 static int rx_dlv_end(rt_pktio_t *e, rx_set_t *s, odp_packet_t out[], int max_out)
 {
+	if (s->chain)
+		return rxc_end(e, s, out, max_out);
 	const uint64_t tk0 = prof_ns();
 	rx_cnt_t *c = &s->cnt;
 	int num_rx = 0, rc = s->derr;
@@ -2348,6 +2423,264 @@ static void rx_finish_start(rt_pktio_t *e, rx_set_t *s)
 	(void)rx_finish_host(e, s, &c, NULL, 0, t2);
 }
 
+/* ------------------------------------------------------- receive chain
+ * One submission per burst (mi_cls_rx_chain_submit): the classification,
+ * the per-frame decisions of rx_dlv_start (parse drop, CoS drop / discard,
+ * destination pool, too long for its pool, queue group) and the delivery
+ * run on the GPU one after the other, with no host step between them.  The
+ * packets the frames go into are taken from the pools before the submit (as
+ * many per pool as the previous bursts used, plus a margin); a burst that
+ * needs more of a pool than it was given is delivered again on the host
+ * (rxc_end), so every outcome stays the reference's
+ * (pktio/loop.c:253-384, pcap.c:299-352).  ODP_AMD_RX_CHAIN=0 turns it off. */
+static int rx_chain_on(void)
+{
+	static int on = -1;
+
+	if (on < 0) {
+		const char *v = getenv("ODP_AMD_RX_CHAIN");
+
+		on = !(v && v[0] == '0');
+	}
+	return on;
+}
+
+/* The chain's table for the current control-plane generation: refilled when
+ * it changed; 0 when the chain can serve this pktio (every pool of the
+ * table page-locked). */
+static int rxc_table(rt_pktio_t *e)
+{
+	const uint64_t g = odp_amd_cls_generation();
+
+	if (e->rxtab && e->rxtab_gen == g)
+		return e->rxtab_ok ? 0 : -1;
+	if (!e->rxtab) {
+		e->rxtab = hmem_alloc(sizeof(mi_cls_rxtab_t), &e->rxtab_pinned);
+		if (!e->rxtab)
+			return -1;
+	}
+	uint64_t tg = 0;
+	uint32_t np = 0;
+	int ok = e->rxtab_pinned &&
+		 odp_amd_cls_rxtab_fill(e->pool, e->rxtab, e->rx_pools, &np, &tg) == 0;
+
+	for (uint32_t k = 0; ok && k < np; k++) {
+		rt_pool_t *rp = rt_pool(e->rx_pools[k]);
+		const int idx = odp_pool_index(e->rx_pools[k]);
+
+		ok = rp && rp->pinned && rp->param.type == ODP_POOL_PACKET && idx >= 0 && idx < 64;
+		if (ok) {
+			e->rxtab->pool_cap[k] = rp->data_cap;
+			e->rxtab->rt_slot[idx] = (uint8_t)(k + 1u);
+		}
+	}
+	if (e->rx_np != np)
+		memset(e->rx_want, 0, sizeof(e->rx_want));   /* first bursts: as many as frames */
+	e->rx_np = np;
+	e->rxtab_gen = tg;
+	e->rxtab_ok = ok && tg == g;
+	return e->rxtab_ok ? 0 : -1;
+}
+
+/* Submit set s's burst as a chain: 1, or 0 when it takes the other path
+ * (nothing done then). */
+static int rxc_submit(rt_pktio_t *e, rx_set_t *s)
+{
+	const uint32_t n = (uint32_t)s->n;
+
+	if (!rx_chain_on() || !gpu_deliver_on() || !e->cls_enabled || e->parse_layer != ODP_PROTO_LAYER_ALL ||
+	    !s->rxc_pinned || !s->dlv_pinned || !s->arr_pinned || n == 0 || n > MI_CLS_DLV_GROUP_MAX ||
+	    (e->drv == DRV_LOOP && !s->pk_pinned) || !mi_cls_host_mapped(s->base) || rxc_table(e))
+		return 0;
+	/* the packets of each pool slot, in the order the frames take them */
+	uint32_t at = 0;
+
+	s->cnp = e->rx_np;
+	for (uint32_t k = 0; k < s->cnp; k++) {
+		uint32_t want = e->rx_want[k] ? e->rx_want[k] : n;
+
+		if (want > n)
+			want = n;
+		if (at + want > s->got_cap)
+			want = s->got_cap - at;
+		s->cpool[k] = e->rx_pools[k];
+		s->cbase[k] = at;
+		s->chave[k] = want ? (uint32_t)rt_packet_alloc_raw(s->cpool[k], 0,
+								   (odp_packet_t *)(void *)(s->got + at),
+								   (int)want) : 0u;
+		at += s->chave[k];
+	}
+	mi_cls_rxc_args_t a;
+
+	memset(&a, 0, sizeof(a));
+	a.base = s->base;
+	a.soff = s->soff;
+	a.slen = s->slen;
+	a.res = s->res;
+	a.n = n;
+	a.layer = (uint32_t)e->parse_layer;
+	a.input = (uint64_t)(uintptr_t)e->hdl;
+	a.headroom = RT_PKT_HEADROOM;
+	a.data_from_meta = rt_data_from_meta();
+	a.tab = e->rxtab;
+	a.got = s->got;
+	memcpy(a.got_base, s->cbase, sizeof(a.got_base));
+	memcpy(a.have, s->chave, sizeof(a.have));
+	if (e->drv == DRV_LOOP) {
+		a.pk = (const uint64_t *)(const void *)s->pk;
+		a.ppool = s->ppool;
+	}
+	a.meta_off = (uint32_t)__builtin_offsetof(pkt_hdr_t, meta);
+	a.dec = s->dec;
+	a.ent = s->cent;
+	a.perm = s->perm;
+	a.gcnt = s->gcnt;
+	a.out = s->rxo;
+	s->gen = odp_amd_cls_generation();
+	s->dgen = e->rxtab_gen;
+	s->dticket = 0;
+	if (odp_amd_cls_rx_chain(e->hdl, s->base, s->bytes, &a, &s->dticket) != 0) {
+		for (uint32_t k = 0; k < s->cnp; k++)
+			rt_packet_return_raw(s->cpool[k], (const odp_packet_t *)(const void *)(s->got + s->cbase[k]),
+					     (int)s->chave[k]);
+		s->dticket = 0;
+		return 0;
+	}
+	s->chain = 1;
+	s->ticket = 0;
+	s->pending = 0;
+	s->delivering = 1;
+	s->derr = 0;
+	return 1;
+}
+
+/* End set s's chain: wait for it, give back the packets no frame took, free
+ * the loop packets that were dropped or copied into another pool, enqueue
+ * (one enqueue per queue group, else runs in arrival order), add the
+ * counters.  A burst that was short of packets, or that the control plane
+ * changed under, is finished on the host instead.  Returns the packets
+ * placed in out[] (none: the classifier is on). */
+static int rxc_end(rt_pktio_t *e, rx_set_t *s, odp_packet_t out[], int max_out)
+{
+	const uint64_t tk0 = prof_ns();
+	int rc = odp_amd_cls_deliver_wait(e->hdl, s->dticket);
+	const mi_cls_rx_out_t *o = s->rxo;
+
+	s->delivering = 0;
+	s->chain = 0;
+	s->dticket = 0;
+	e->prof[9] += prof_ns() - tk0;
+	if (!rc) {
+		/* the next bursts' packets per slot: this one's need plus a margin */
+		for (uint32_t k = 0; k < s->cnp && k < e->rx_np; k++)
+			e->rx_want[k] = o->need[k] + o->need[k] / 4u + 32u;
+	}
+	if (rc || o->short_pool || s->dgen != odp_amd_cls_generation()) {
+		/* every packet taken for the burst back; the host path then
+		 * decides, allocates and delivers from the records (the classify
+		 * records are valid; a control-plane change re-classifies) */
+		for (uint32_t k = 0; k < s->cnp; k++)
+			rt_packet_return_raw(s->cpool[k], (const odp_packet_t *)(const void *)(s->got + s->cbase[k]),
+					     (int)s->chave[k]);
+		if (rc) {
+			rx_drop(e, s, rc);
+			return 0;
+		}
+		s->pending = 1;
+		return rx_finish(e, s, out, max_out);
+	}
+	const uint64_t tk1 = prof_ns();
+
+	for (uint32_t k = 0; k < s->cnp; k++)
+		if (o->used[k] < s->chave[k])
+			rt_packet_return_raw(s->cpool[k],
+					     (const odp_packet_t *)(const void *)(s->got + s->cbase[k] + o->used[k]),
+					     (int)(s->chave[k] - o->used[k]));
+	if (e->drv == DRV_LOOP) {
+		/* loop packets not delivered in their own buffer: dropped,
+		 * discarded, or copied into a packet of their CoS pool */
+		for (int i = 0; i < s->n; i++)
+			if ((s->dec[i] & 3u) != MI_CLS_RXF_INPLACE)
+				odp_packet_free(s->pk[i]);
+	}
+	odp_packet_t *tmp = s->tmp;
+
+	if (!tmp || s->tmp_cap < s->n_cap) {
+		free(s->tmp);
+		s->tmp = malloc(s->n_cap * (sizeof(odp_packet_t) + 1u));
+		s->tmp_cap = s->tmp ? s->n_cap : 0;
+		tmp = s->tmp;
+	}
+	if ((e->rxtab->flags & MI_CLS_RXT_GROUP) && tmp) {
+		/* group g holds frames perm[at .. at + gcnt[g]) of the queue whose
+		 * entries carry group g; queue stats per CoS of the queue */
+		uint32_t at = 0;
+
+		for (int g = 0; g < MI_CLS_DLV_GROUPS; g++) {
+			const uint32_t num = s->gcnt[g];
+
+			if (!num)
+				continue;
+			const uint32_t i0 = s->perm[at];
+			const mi_cls_result_t *r0 = &s->res[i0];
+			const odp_queue_t q = (odp_queue_t)(uintptr_t)
+				e->rxtab->qh[e->rxtab->cos_q0[r0->cos] + r0->queue];
+			uint64_t ok[256], bad[256];
+			uint8_t seen[256], cl[256];
+			int ncos = 0;
+
+			for (uint32_t k = 0; k < num; k++)
+				tmp[k] = (odp_packet_t)(uintptr_t)s->cent[s->perm[at + k]];
+			int r = odp_queue_enq_multi(q, (const odp_event_t *)(void *)tmp, (int)num);
+
+			if (r < 0)
+				r = 0;
+			if ((uint32_t)r != num)
+				odp_packet_free_multi(&tmp[r], (int)num - r);
+			memset(seen, 0, sizeof(seen));
+			for (uint32_t k = 0; k < num; k++) {
+				const uint32_t cos = s->res[s->perm[at + k]].cos;
+
+				if (!seen[cos]) {
+					seen[cos] = 1;
+					cl[ncos++] = (uint8_t)cos;
+					ok[cos] = 0;
+					bad[cos] = 0;
+				}
+				if (k < (uint32_t)r)
+					ok[cos]++;
+				else
+					bad[cos]++;
+			}
+			for (int j = 0; j < ncos; j++)
+				odp_amd_cls_queue_stats_add(cl[j], cos_slot_of(cl[j], q), ok[cl[j]], bad[cl[j]]);
+			at += num;
+		}
+	} else {
+		/* runs of equal (queue, CoS) in arrival order (_odp_cls_enq) */
+		int nd = 0;
+
+		for (int i = 0; i < s->n; i++)
+			if (s->cent[i])
+				s->pk[nd++] = (odp_packet_t)(uintptr_t)s->cent[i];
+		if (tmp)
+			rx_enqueue(s->pk, nd, tmp, (uint8_t *)(void *)(tmp + s->tmp_cap));
+		else
+			for (int i = 0; i < nd; i++)
+				cos_enq_run(&s->pk[i], 1);
+	}
+	if (o->in_errors)
+		odp_atomic_add_u64(&e->in_errors, o->in_errors);
+	if (o->in_discards)
+		odp_atomic_add_u64(&e->in_discards, o->in_discards);
+	odp_atomic_add_u64(&e->in_octets, o->octets);
+	odp_atomic_add_u64(&e->in_packets, o->packets);
+	e->prof[10] += prof_ns() - tk1;
+	(void)out;
+	(void)max_out;
+	return 0;
+}
+
 /* Set of age k: staged k calls ago (age 0: this call). */
 static rx_set_t *rx_age(rt_pktio_t *e, int k)
 {
@@ -2410,7 +2743,7 @@ static int pktio_recv(rt_pktio_t *e, odp_packet_t out[], int max_out)
 	s->n = n > 0 ? n : 0;
 	if (n > 0) {
 		e->prof[3]++;
-		if (rx_classify(e, s, pipe))
+		if (!(pipe && rxc_submit(e, s)) && rx_classify(e, s, pipe))
 			n = 0;
 		e->prof[1] += prof_ns() - t1;
 	}
@@ -2421,7 +2754,7 @@ static int pktio_recv(rt_pktio_t *e, odp_packet_t out[], int max_out)
 		num_rx += rx_dlv_end(e, z, out, max_out);
 	/* only a burst really in flight streams (a multi-GPU pktio's submit
 	 * completes before it returns: ticket 0) */
-	if (n > 0 && pipe && s->ticket && rx_more(e)) {
+	if (n > 0 && pipe && (s->ticket || s->chain) && rx_more(e)) {
 		rx_set_t *q = rx_age(e, RX_CLS_DEPTH);
 
 		if (q->pending)
@@ -2439,8 +2772,12 @@ static int pktio_recv(rt_pktio_t *e, odp_packet_t out[], int max_out)
 		if (b->pending)
 			num_rx += rx_finish(e, b, out + num_rx, max_out - num_rx);
 	}
-	if (n > 0)
-		num_rx += rx_finish(e, s, out + num_rx, max_out - num_rx);
+	if (n > 0) {
+		if (s->delivering)
+			num_rx += rx_dlv_end(e, s, out + num_rx, max_out - num_rx);
+		else
+			num_rx += rx_finish(e, s, out + num_rx, max_out - num_rx);
+	}
 	return num_rx;
 }
 

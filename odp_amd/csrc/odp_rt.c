@@ -958,6 +958,30 @@ int rt_packet_alloc_raw(odp_pool_t pool, uint32_t len, odp_packet_t pkt[], int n
 	return pool_alloc(p, (ev_hdr_t **)(void *)pkt, num);
 }
 
+/* Packets of one pool back to it at once (taken with rt_packet_alloc_raw and
+ * not used): into the calling thread's cache while it has room, the rest
+ * onto the pool's stack in one locked copy. */
+void rt_packet_return_raw(odp_pool_t pool, const odp_packet_t pkt[], int num)
+{
+	rt_pool_t *p = rt_pool(pool);
+
+	if (!p || num <= 0)
+		return;
+	ev_hdr_t *const *e = (ev_hdr_t *const *)(const void *)pkt;
+	pool_cache_t *c = pool_cache(p);
+
+	if (c) {
+		const int room = PC_SIZE - c->n;
+		const int k = num < room ? num : room;
+
+		memcpy(c->e + c->n, e, (size_t)k * sizeof(ev_hdr_t *));
+		c->n += k;
+		e += k;
+		num -= k;
+	}
+	pool_give(p, e, num);
+}
+
 void rt_packet_init(odp_packet_t pkt, uint32_t len)
 {
 	pkt_init(rt_pkt_hdr(pkt), len);

@@ -136,6 +136,8 @@ uint32_t rt_pool_avail(odp_pool_t pool);
  * count taken */
 int rt_packet_alloc_raw(odp_pool_t pool, uint32_t len, odp_packet_t pkt[], int num);
 void rt_packet_init(odp_packet_t pkt, uint32_t len);
+/* packets taken with rt_packet_alloc_raw and not used, back to their pool */
+void rt_packet_return_raw(odp_pool_t pool, const odp_packet_t pkt[], int num);
 int rt_queue_enq_multi(rt_queue_t *q, const odp_event_t ev[], int num);
 int rt_queue_deq_multi_raw(rt_queue_t *q, odp_event_t ev[], int num);
 int rt_thread_id(void);
