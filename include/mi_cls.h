@@ -414,6 +414,7 @@ typedef struct mi_cls_rxtab {
 	uint8_t  cos_pool[256];       /* CoS index -> pool slot                     */
 	uint8_t  cos_nq[256];         /* queues of the CoS                          */
 	uint16_t cos_q0[256];         /* its first entry of qh / qg                 */
+	uint8_t  rt_pinned[64];       /* runtime pool index -> 1: page-locked pool   */
 	uint64_t qh[MI_CLS_RX_QENT];  /* odp_queue_t per (CoS, queue slot)          */
 	uint8_t  qg[MI_CLS_RX_QENT];  /* its queue group 0..63 (MI_CLS_RXT_GROUP)   */
 } mi_cls_rxtab_t;
@@ -423,7 +424,9 @@ typedef struct mi_cls_rx_out {
 	uint32_t used[MI_CLS_RX_POOLS];   /* packets taken of each slot              */
 	uint32_t need[MI_CLS_RX_POOLS];   /* frames that wanted a packet of the slot */
 	uint32_t short_pool;          /* 1: a slot had too few packets (host redo)  */
-	uint32_t rsv[3];
+	uint32_t not_in_place;        /* loop staging (stage): a packet outside the  */
+				      /* page-locked arena (host redo)              */
+	uint32_t rsv[2];
 } mi_cls_rx_out_t;
 
 /* Frame decision word (dec[i]): fate in bits 0-1, pool slot in bits 2-6,
@@ -438,7 +441,7 @@ typedef struct mi_cls_rxc_args {
 	const uint8_t *base;          /* the burst's frames (soff[i] from here)     */
 	const uint32_t *soff;
 	const uint16_t *slen;
-	mi_cls_result_t *res;         /* records (written by the chain's classify)  */
+	mi_cls_result_t *res;         /* records (every frame's, when the ticket is done) */
 	uint32_t n;                   /* frames (<= MI_CLS_DLV_GROUP_MAX)           */
 	uint32_t layer;               /* parser layer (ODP_PROTO_LAYER_L2..ALL)     */
 	uint64_t input;               /* odp_pktio_t written into meta              */
@@ -451,7 +454,10 @@ typedef struct mi_cls_rxc_args {
 	const uint8_t *ppool;         /* loop: its runtime pool index + 1           */
 	const uint16_t *pdoff;        /* loop: its headroom                         */
 	uint32_t meta_off;            /* bytes from a packet handle to its meta     */
-	uint32_t rsv;
+	uint32_t stage;               /* loop: the device builds soff / slen / ppool */
+				      /* from the packets' headers (pk) first       */
+	uint16_t head_off;            /* stage: offset of a header's buffer pointer */
+	uint16_t pool_off;            /* stage: offset of its u16 pool index        */
 	/* outputs */
 	uint32_t *dec;                /* per frame: decision word                   */
 	uint64_t *ent;                /* per frame: the delivered packet (0: none)  */

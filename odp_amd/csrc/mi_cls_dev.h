@@ -13,6 +13,14 @@
 //   odp_classification.c:1624-1771  match_pmr_cos / cls_select_cos / _odp_cls_classify_packet
 //   odp_classification.c:395-405, 1773-1839 + protocols/thash.h:82-99  hash-queue pick
 //
+// Measurement hooks (phase-floor variants built with tools/ab.py and
+// `python -m odp_amd._build DIR DIAG_...`; never in a shipped build, their
+// records are wrong on purpose): DIAG_NOSTAGE (no window loads after a
+// wave's first tile: the compute-only floor), DIAG_STAGEONLY (windows and
+// records only), DIAG_PARSEONLY (no classification), DIAG_MAXROUND=n (the
+// descent stops after n rounds), DIAG_DESCENTONLY (no final-CoS step),
+// DIAG_CK_NOSUM / DIAG_CK_NOSCTP / DIAG_CK_OK (checksum parts left out).
+//
 // Design (MI355X-first, not a translation; DESIGN.md has the details):
 //   * one wavefront owns 64 consecutive packets (a tile, one packet per lane)
 //     and loops over its tiles with the next tile's header loads in flight;
@@ -46,21 +54,12 @@
 #include <type_traits>
 
 #define WAVE 64
-#ifndef WIN
-#define WIN 96             // staged header window, bytes (96 or 128)
-#endif
+#define WIN 96             // staged header window, bytes
 #define WROWS (WIN / 4 + 1)     // LDS dword rows per wave window (+1 zero row)
 #define RS 66                   // LDS row stride of a window, dwords (see load_window)
 #define NPIECE (WIN / 16)       // 16-B pieces per window
-#ifndef MIN_WAVES_PER_EU
-#define MIN_WAVES_PER_EU 4
-#endif
-#ifndef LOAD_AUX
+#define MIN_WAVES_PER_EU 4   // waves per SIMD of the 4-wave block shapes (the VGPR budget)
 #define LOAD_AUX 2          // cache policy of the packet-window loads: nt (read once)
-#endif
-#ifndef PREFETCH
-#define PREFETCH 1          // software-pipeline the next tile's loads
-#endif
 #define MAX_STATS_COS 256
 
 // ---------------------------------------------------------------- flags
@@ -560,9 +559,7 @@ __device__ __forceinline__ uint32_t wave_scan_add(uint32_t v, uint32_t lane)
 // prefix sum over the round gives each owner its pieces' total as the
 // difference of two prefix values.  Returns the lane's own sum (congruent
 // mod 0xffff, < 2^32).
-#ifndef CK_HALVES
-#define CK_HALVES 1         // pieces per lane per round of ck_sum_wave (A/B: 2, 3 slower)
-#endif
+#define CK_HALVES 1         // pieces per lane per round of ck_sum_wave (2, 3 measured slower)
 __device__ __forceinline__ uint32_t ck_sum_wave(__amdgpu_buffer_rsrc_t rs, uint32_t base,
 						uint32_t prm, uint32_t cnt, uint32_t lane)
 {
@@ -660,9 +657,7 @@ __device__ __forceinline__ uint32_t ck_sum_wave(__amdgpu_buffer_rsrc_t rs, uint3
 // frame's 16-B rounding, the batch contract), the words funnel-shifted when
 // l4 is 2 mod 4; the last 0-3 bytes one at a time.  Returns the finished
 // (inverted) CRC.
-#ifndef CK_AHEAD
 #define CK_AHEAD 4          // 16-B pieces in flight per lane in sctp_crc
-#endif
 __device__ __forceinline__ uint32_t sctp_crc(const Pkt &k, __amdgpu_buffer_rsrc_t rs, uint32_t boff,
 					     uint32_t l4, const uint32_t *tab)
 {
@@ -875,10 +870,28 @@ __device__ __forceinline__ void l4_chksum(const Pkt &k, Parsed &p, uint32_t opt,
 			else              // odp_cpu_to_be_16(frame_len - l4), IPPROTO_TCP << 8
 				s += (((len - l4) & 0xffu) << 8) + (((len - l4) >> 8) & 0xffu) + (6u << 8);
 			// the parse guarantees l4 + 8 <= len (UDP) / l4 + 20 <= len (TCP)
-			const uint32_t p0 = l4 & ~63u;
-			cnt = (len - p0 + 63u) >> 6;
-			base = boff + p0;
-			prm = (l4 - p0) | ((len - p0) << 6);
+			if (l4 >= 32u && l4 < 64u) {
+				// bytes [l4, 64) are in the staged window (bytes past the
+				// frame read 0 there): summed from LDS, so the wave's
+				// pieces start at byte 64 and a frame of at most 64 B
+				// reads nothing more (dword rows 8-15, the first one from
+				// l4's, its lower half cut when l4 is 2 mod 4: congruent
+				// modulo 0xffff either way)
+#pragma unroll
+				for (uint32_t d = 8; d < 16; ++d) {
+					const uint32_t w = k.w[d * RS];
+					const uint32_t m = 4u * d + 4u <= l4 ? 0u : (4u * d < l4 ? 0xffff0000u : ~0u);
+					s += w & m;
+				}
+				cnt = len > 64u ? (len - 64u + 63u) >> 6 : 0u;
+				base = boff + 64u;
+				prm = len > 64u ? (len - 64u) << 6 : 0u;
+			} else {
+				const uint32_t p0 = l4 & ~63u;
+				cnt = (len - p0 + 63u) >> 6;
+				base = boff + p0;
+				prm = (l4 - p0) | ((len - p0) << 6);
+			}
 		}
 #ifndef DIAG_CK_NOSUM
 		s += ck_sum_wave(rs, base, prm, cnt, lane);
@@ -2124,22 +2137,6 @@ __device__ __forceinline__ void linear_scan(cword_t prog, uint32_t rec0, uint32_
 		done = ok ? 1u : done;
 	}
 }
-// Diagnostic build only (-DDIAG_STAMPS): per-phase cycle sums per wave,
-// written to a debug buffer nobody else reads (cdna_hip_programming.md §7).
-#ifdef DIAG_STAMPS
-#define NSTAMP 8
-#define STAMP(i)                                                                   \
-	do {                                                                       \
-		__builtin_amdgcn_sched_barrier(0);                                 \
-		unsigned long long t_;                                             \
-		asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_) :: "memory"); \
-		__builtin_amdgcn_sched_barrier(0);                                 \
-		st_acc[i] += t_ - st_last;                                         \
-		st_last = t_;                                                      \
-	} while (0)
-#else
-#define STAMP(i) do { } while (0)
-#endif
 
 // ------------------------------------------------------------------ kernel
 struct KArgs {
@@ -2150,7 +2147,6 @@ struct KArgs {
 	const uint32_t *dev;         // device rule program (constant address space)
 	mi_cls_result_t *out;
 	unsigned long long *stats;   // MAX_STATS_COS counters, or NULL
-	unsigned long long *diag;    // DIAG_STAMPS builds only
 	uint32_t stats_mask[8];
 	uint32_t opt;                // pktin options (OPT_*), 0: none
 	// window hint across launches of a context: a wave of block 0 whose
@@ -2166,7 +2162,7 @@ __device__ __forceinline__ bool stats_bit(const KArgs &a, uint32_t c)
 	return c < MAX_STATS_COS && ((a.stats_mask[c >> 5] >> (c & 31u)) & 1u);
 }
 
-static_assert(NPIECE == 8 || NPIECE == 6, "WIN must be 96 or 128");
+static_assert(NPIECE == 6, "WIN is 96");
 #define NB (NPIECE - 4)         // upper pieces (phase B)
 
 // Issue the loads of a tile's header windows (64 packets, per-lane
@@ -2269,34 +2265,21 @@ __device__ __forceinline__ void zero_tail(uint32_t *W, uint32_t lane, uint32_t l
 	W[min(r0 + 2u, (uint32_t)(WIN / 4)) * RS + lane] = 0u;
 }
 
-// Packet descriptors are read once; DESC_NT=1 loads them nontemporal (A/B:
-// within noise, so the default keeps plain loads).
-#ifndef DESC_NT
-#define DESC_NT 0
-#endif
+// Packet descriptors are read once (nontemporal loads measured within
+// noise: plain loads).
 template <typename T> __device__ __forceinline__ uint32_t ld_desc(const T *p)
 {
-	if (DESC_NT)
-		return (uint32_t)__builtin_nontemporal_load(p);
 	return (uint32_t)*p;
 }
 
 // One 16-B result record (a coalesced dwordx4 store per lane), nontemporal:
 // the records are not read again by this kernel, and streaming them out
 // instead of leaving 16 MB of dirty lines in L2 for the end-of-kernel
-// release cut 4-6 % per launch on every config (REC_NT=0: cached stores,
-// for A/B runs).
-#ifndef REC_NT
-#define REC_NT 1
-#endif
+// release cut 4-6 % per launch on every config (cached stores measured).
 __device__ __forceinline__ void store_rec(mi_cls_result_t *dst, uint4 r)
 {
-	if (REC_NT) {
-		u32x4 v = { r.x, r.y, r.z, r.w };
-		__builtin_nontemporal_store(v, (u32x4 *)dst);
-	} else {
-		*(uint4 *)dst = r;
-	}
+	u32x4 v = { r.x, r.y, r.z, r.w };
+	__builtin_nontemporal_store(v, (u32x4 *)dst);
 }
 
 // Make this wave's LDS writes visible to its own later LDS reads by other
@@ -2354,10 +2337,6 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 	const uint32_t lane = threadIdx.x & (WAVE - 1);
 	const uint32_t wave = threadIdx.x >> 6;
 	uint32_t *W = s_win + wave * RS * WROWS;
-#ifdef DIAG_STAMPS
-	unsigned long long st_acc[NSTAMP] = { 0 }, st_last;
-	asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_last) :: "memory");
-#endif
 
 	const cword_t dev = (cword_t)a.dev;
 	const int32_t def_cos = (int32_t)dev[DH_DEFAULT];
@@ -2406,13 +2385,7 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 	// window predictor: stage bytes 64..WIN-1 of long frames only while the
 	// frames of the last parsed tile needed them (the fields of its rule
 	// program and its parse reach past byte 64); the first tiles stage them
-#if defined(DIAG_FORCE_LO)
-	bool want_hi = false;     // diagnostic: 64-B windows from the first tile
-#elif defined(DIAG_FORCE_HI)
-	bool want_hi = true;
-#else
 	bool want_hi = a.hint == nullptr || *(const uint32_t *)a.hint + 1u == a.seq;
-#endif
 	// PLH (tree kernels without pktin options): bytes 64..WIN-1 are staged
 	// per lane, for the frames whose parse or program fields reach past byte
 	// 64 (a QinQ IPv6 frame's ports, an IPv6 TCP data offset), after the
@@ -2458,7 +2431,6 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 	for (uint32_t r = WIN / 4; r < WROWS; ++r)
 		W[r * RS + lane] = 0u;   // pad / zero rows: always zero
 	__syncthreads();
-	STAMP(5);   // block setup (hot-region copy) done
 
 	uint4 prev_rec = make_uint4(0, 0, 0, 0);
 	uint32_t prev_pi = 0;
@@ -2466,11 +2438,6 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 	for (; tile < nt; tile += tstride) {
 		const uint32_t pi = tile * WAVE + lane;
 		const bool valid = pi < a.n;
-		if (!PREFETCH && tile != blockIdx.x * NW + wave) {
-			d_off = valid ? a.off[pi] : 0u;
-			d_len = valid ? (uint32_t)a.len[pi] : 0u;
-			d_hi = load_window(rs, d_off, d_len, lane, d, want_hi, d_win);
-		}
 		const uint32_t my_off = d_off, my_len = d_len;
 		my_win = d_win;
 
@@ -2483,7 +2450,6 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 			store_rec(a.out + prev_pi, prev_rec);
 		prev_valid = false;
 
-		STAMP(0);   // data of this tile landed in LDS
 		// advance the pipeline: data of tile+stride, descriptors of tile+2*stride
 		// (PLH: after the parse, behind this tile's far loads in the vmcnt
 		// queue, so waiting for those never waits for the next tile's window)
@@ -2493,7 +2459,7 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 			// first tile (no window loads after it): the compute-only floor
 			if (false) {
 #else
-			if (PREFETCH) {
+			{
 #endif
 				d_off = n_off;
 				d_len = n_len;
@@ -2533,7 +2499,6 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 		k.len = my_len;
 		k.win = PLH ? 64u : my_win;
 
-		STAMP(1);   // next tile's loads issued
 		Parsed p;
 		bool dfr = false;
 		if constexpr (!CK) {
@@ -2614,11 +2579,7 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 			// one's frames needed them
 			// (reading a TCP data offset past a 64-B window from HBM instead
 			// of staging 96-B windows measured 3-6 % slower on configs 3-5)
-#ifdef DIAG_FORCE_HI
-			want_hi = true;
-#else
 			want_hi = __ballot(valid && my_len > 64u && need > 64u) != 0ull;
-#endif
 			saw_hi = saw_hi || want_hi;
 		}
 		// PLH: the far pieces into the window (rows 16..), the lanes' windows
@@ -2677,7 +2638,6 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 		int32_t cur = perr ? err_cos : def_cos;
 		uint32_t pend = (ok_parse && !perr && def_cos >= 0 && def_valid) ? 1u : 0u;
 
-		STAMP(2);   // parsed, start CoS selected
 		// ---- CoS descent (match_pmr_cos, :1624-1667).  Each round moves
 		// pending lanes one hop: the CoS of the first pending lane is
 		// evaluated by every lane sitting on it (bit-vector or linear engine,
@@ -2871,7 +2831,6 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 			advance(handled | grp, hit, nxt, nmark, nleaf);
 		}
 
-		STAMP(3);   // descent done
 #ifdef DIAG_DESCENTONLY
 		if (valid) {
 			uint4 rec;
@@ -2920,23 +2879,13 @@ __global__ __launch_bounds__(NW * WAVE, waves_per_eu(NW)) void mi_cls_kernel(KAr
 		prev_rec.w = (p.l3 & 0xffffu) | ((p.l4 & 0xffffu) << 16);
 		prev_pi = pi;
 		prev_valid = valid;
-		STAMP(4);   // outcome computed, record stored
 	}
-	STAMP(7);   // loop left
 	if (prev_valid)
 		store_rec(a.out + prev_pi, prev_rec);
 	// the waves of block 0 are the sample that sets the hint: stores to one
 	// address serialise, so never one per wave
 	if (saw_hi && a.hint && lane == 0 && blockIdx.x == 0)
 		*a.hint = a.seq;
-	STAMP(6);   // last record issued
-#ifdef DIAG_STAMPS
-	if (lane == 0 && a.diag) {
-		for (int i = 0; i < NSTAMP; ++i)
-			atomicAdd(a.diag + i, st_acc[i]);
-		atomicAdd(a.diag + NSTAMP, 1ull);
-	}
-#endif
 
 	if (stats_on) {
 		__syncthreads();
@@ -2964,9 +2913,21 @@ int mi_cls_launch_ck(int nw, bool lt, bool div, unsigned grid, size_t dyn, hipSt
 int mi_cls_launch_deliver(unsigned grid, hipStream_t st, const mi_cls_dlv_args_t &h);
 // receive chain (mi_cls_kd.hip): decisions on `cls` after the burst's
 // classification, `dep` recorded there, the delivery on `dlv` after it;
-// preload: resolve both kernels only
+// preload: resolve both kernels only.  The chain's device-resident
+// per-burst arrays (the context's, one set per ticket slot): the records
+// (the classification writes them here; the delivery copies them to
+// args.res), the decision words and each enqueued frame's queue handle --
+// the decide and delivery kernels read these from HBM, not over the host
+// link.
+struct mi_cls_rxdev_t {
+	mi_cls_result_t *res;
+	uint32_t *dec;
+	uint64_t *dq;
+};
 int mi_cls_launch_rx_chain(hipStream_t cls, hipStream_t dlv, hipEvent_t dep, const mi_cls_rxc_args_t &a,
-			   bool preload);
+			   const mi_cls_rxdev_t &d, bool preload);
+// loop receive staging on the device (mi_cls_rxc_args_t.stage)
+int mi_cls_launch_rx_stage(hipStream_t st, const mi_cls_rxc_args_t &a, uint64_t bytes, bool preload);
 
 // Every launcher goes through mi_launch.  grid == 0 launches nothing: it
 // resolves the instantiation on the current device (hipFuncGetAttributes

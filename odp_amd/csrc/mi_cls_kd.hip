@@ -250,52 +250,99 @@ int mi_cls_launch_deliver(unsigned grid, hipStream_t st, const mi_cls_dlv_args_t
 #define RXD_WAVES (RXD_THREADS / WAVE)
 
 // Decisions of frames [0, n) in arrival order: fate, pool slot, the frame's
-// rank among its slot's frames (the got packet it takes), queue group, and
-// the packet it is delivered in; the pktio counters; the stable grouping by
-// queue (as dlv_group); `short_pool` when a slot has too few packets.
-__global__ __launch_bounds__(RXD_THREADS) void mi_cls_rx_decide_kernel(mi_cls_rxc_args_t a)
+// rank among its slot's frames (which packet of the slot it takes), queue
+// group; the pktio counters; the stable grouping by queue (as dlv_group);
+// `short_pool` when a slot has too few packets.  One block.  Latency rules
+// it, not bytes: every load of the inputs (records in HBM; lengths, pools and
+// the table in host memory) is issued before any is used, each thread's
+// frames stay in registers (fully unrolled, constant indexes: nothing in
+// scratch), and every store goes out after the last barrier -- a barrier
+// waits for the block's outstanding stores, which to host memory are a
+// host-link round trip each (the first version's 26 barriers behind host
+// stores took 84 us per 4096-frame burst).
+#define RXD_PER 8   // frames per thread (MI_CLS_DLV_GROUP_MAX / RXD_THREADS)
+static_assert(RXD_PER * RXD_THREADS == MI_CLS_DLV_GROUP_MAX, "one block holds a burst");
+__global__ __launch_bounds__(RXD_THREADS) void mi_cls_rx_decide_kernel(mi_cls_rxc_args_t a, mi_cls_rxdev_t d)
 {
 	__shared__ uint8_t s_q[MI_CLS_DLV_GROUP_MAX];
 	__shared__ uint32_t s_w[RXD_WAVES][MI_CLS_RX_POOLS];   // per wave: fresh frames per slot
 	__shared__ uint32_t s_base[MI_CLS_RX_POOLS];           // frames of each slot so far
 	__shared__ uint32_t s_gw[RXD_WAVES][MI_CLS_DLV_GROUPS];
 	__shared__ uint32_t s_gcnt[MI_CLS_DLV_GROUPS], s_gpos[MI_CLS_DLV_GROUPS];
-	__shared__ unsigned long long s_ctr[4];
+	__shared__ uint32_t s_ctr[4];
+	__shared__ uint8_t s_cpool[256], s_rts[64], s_qg[MI_CLS_RX_QENT];
+	__shared__ uint16_t s_q0[256];
+	__shared__ uint64_t s_qh[MI_CLS_RX_QENT];
+	__shared__ uint32_t s_cap[MI_CLS_RX_POOLS], s_have[MI_CLS_RX_POOLS];
 	const uint32_t t = threadIdx.x, lane = t & (WAVE - 1), wave = t / WAVE;
 	const mi_cls_rxtab_t &tab = *a.tab;
 	const bool group = (tab.flags & MI_CLS_RXT_GROUP) != 0u;
 	const unsigned long long lt = lane ? (~0ull >> (64u - lane)) : 0ull;
-	if (t < MI_CLS_RX_POOLS)
-		s_base[t] = 0u;
-	if (t < MI_CLS_DLV_GROUPS)
-		s_gcnt[t] = 0u;
-	if (t < 4)
-		s_ctr[t] = 0ull;
+	const uint32_t n = a.n, nc = (n + RXD_THREADS - 1u) / RXD_THREADS;
+	// this thread's frames t, t + 1024, ..: unconditional loads (indexes
+	// clamped into the burst, a valid byte array when there is no ppool), so
+	// no branch makes the compiler wait for one before the next is issued
+	mi_cls_result_t r[RXD_PER];
+	uint32_t len[RXD_PER], pp[RXD_PER];
+	const uint8_t *ppa = a.pk ? a.ppool : (const uint8_t *)a.slen;
+#pragma unroll
+	for (uint32_t c = 0; c < RXD_PER; ++c) {
+		const uint32_t i = min(c * RXD_THREADS + t, n - 1u);
+		r[c] = d.res[i];
+		len[c] = a.slen[i];
+		pp[c] = ppa[i];
+	}
+	// the table's words, also unconditional (wrapped indexes); every thread
+	// stores (threads with equal wrapped indexes store the same word): no
+	// branch the compiler could sink the loads into
+	static_assert(MI_CLS_RX_QENT == RXD_THREADS, "one queue entry per thread");
+	{
+		const uint8_t cp = tab.cos_pool[t & 255u], qg = tab.qg[t], rs = tab.rt_slot[t & 63u];
+		const uint64_t qh = tab.qh[t];
+		const uint16_t q0 = tab.cos_q0[t & 255u];
+		const uint32_t cap = tab.pool_cap[t & (MI_CLS_RX_POOLS - 1u)];
+		const uint32_t hv = a.have[t & (MI_CLS_RX_POOLS - 1u)];
+		s_qg[t] = qg;
+		s_qh[t] = qh;
+		s_cpool[t & 255u] = cp;
+		s_q0[t & 255u] = q0;
+		s_rts[t & 63u] = rs;
+		s_cap[t & (MI_CLS_RX_POOLS - 1u)] = cap;
+		s_have[t & (MI_CLS_RX_POOLS - 1u)] = hv;
+		s_base[t & (MI_CLS_RX_POOLS - 1u)] = 0u;
+		s_gcnt[t & (MI_CLS_DLV_GROUPS - 1u)] = 0u;
+		s_ctr[t & 3u] = 0u;
+	}
 	__syncthreads();
-	unsigned long long errs = 0, disc = 0, pkts = 0, octs = 0;
-	for (uint32_t c0 = 0; c0 < a.n; c0 += RXD_THREADS) {
-		const uint32_t i = c0 + t;
-		const bool in = i < a.n;
-		mi_cls_result_t r = {};
-		if (in)
-			r = a.res[i];
-		const uint32_t len = in ? a.slen[i] : 0u;
+	uint32_t w[RXD_PER], qe[RXD_PER], pos[RXD_PER];
+	uint32_t errs = 0, disc = 0, pkts = 0, octs = 0;
+#pragma unroll
+	for (uint32_t c = 0; c < RXD_PER; ++c) {
+		w[c] = 0u;
+		qe[c] = 0u;
+		pos[c] = ~0u;
+		if (c >= nc)   // uniform
+			continue;
+		const uint32_t i = c * RXD_THREADS + t;
+		const bool in = i < n;
+		const uint32_t p = a.pk ? pp[c] : 0u;
 		uint32_t fate = MI_CLS_RXF_DROP, k = 0u;
 		if (in) {
-			errs += (r.err != 0u || r.outcome == MI_CLS_OUT_PARSE_DROP) ? 1u : 0u;
-			if (r.outcome == MI_CLS_OUT_DISCARD || r.outcome == MI_CLS_OUT_LOOP) {
+			errs += (r[c].err != 0u || r[c].outcome == MI_CLS_OUT_PARSE_DROP) ? 1u : 0u;
+			if (r[c].outcome == MI_CLS_OUT_DISCARD || r[c].outcome == MI_CLS_OUT_LOOP) {
 				fate = MI_CLS_RXF_DISCARD;
-			} else if (r.outcome == MI_CLS_OUT_ENQ) {
-				k = tab.cos_pool[r.cos];
-				const uint32_t own = a.pk && a.ppool[i] ? tab.rt_slot[a.ppool[i] - 1u] : 0u;
+			} else if (r[c].outcome == MI_CLS_OUT_ENQ) {
+				k = s_cpool[r[c].cos];
+				const uint32_t own = p ? s_rts[(p - 1u) & 63u] : 0u;
 				if (own != 0u && own - 1u == k)
 					fate = MI_CLS_RXF_INPLACE;
-				else if (len > tab.pool_cap[k])
+				else if (len[c] > s_cap[k & (MI_CLS_RX_POOLS - 1u)])
 					fate = MI_CLS_RXF_DISCARD;   // odp_packet_alloc fails
 				else
 					fate = MI_CLS_RXF_FRESH;
 			}
 		}
+		k &= MI_CLS_RX_POOLS - 1u;
 		// rank among the slot's fresh frames: the wave's lanes before this
 		// one (a ballot per slot present in the wave), then the earlier
 		// waves of the chunk and the earlier chunks
@@ -321,44 +368,119 @@ __global__ __launch_bounds__(RXD_THREADS) void mi_cls_rx_decide_kernel(mi_cls_rx
 		}
 		__syncthreads();
 		if (fr) {
-			for (uint32_t w = 0; w < wave; ++w)
-				rank += s_w[w][k];
+			for (uint32_t v = 0; v < wave; ++v)
+				rank += s_w[v][k];
 			rank += s_base[k];
 		}
-		const bool got = fr && rank < a.have[k];
-		const bool dlv = got || fate == MI_CLS_RXF_INPLACE;
+		const bool dlv = (fr && rank < s_have[k]) || fate == MI_CLS_RXF_INPLACE;
 		if (fate == MI_CLS_RXF_DISCARD)
 			++disc;
-		if (dlv && r.err == 0u) {
+		if (dlv && r[c].err == 0u) {
 			++pkts;
-			octs += len;
+			octs += len[c];
 		}
-		const uint32_t qe = in && r.outcome == MI_CLS_OUT_ENQ ? tab.cos_q0[r.cos] + r.queue : 0u;
-		const uint32_t qid = dlv && group ? tab.qg[qe] : 0x7Fu;
-		if (in) {
-			a.dec[i] = fate | (k << 2) | ((qid & 0x7Fu) << 8) | (min(rank, 0xFFFFu) << 16);
-			a.ent[i] = got ? a.got[a.got_base[k] + rank] : (fate == MI_CLS_RXF_INPLACE ? a.pk[i] : 0ull);
+		qe[c] = min(in && r[c].outcome == MI_CLS_OUT_ENQ ? s_q0[r[c].cos] + r[c].queue : 0u,
+			    (uint32_t)MI_CLS_RX_QENT - 1u);
+		const uint32_t qid = dlv && group ? s_qg[qe[c]] : 0x7Fu;
+		w[c] = fate | (k << 2) | ((qid & 0x7Fu) << 8) | (min(rank, 0xFFFFu) << 16);
+		if (in)
 			s_q[i] = (uint8_t)(qid < MI_CLS_DLV_GROUPS ? qid : 0xFFu);
-		}
 		__syncthreads();
 		if (t < MI_CLS_RX_POOLS) {
 			uint32_t all = 0;
-			for (uint32_t w = 0; w < RXD_WAVES; ++w)
-				all += s_w[w][t];
+			for (uint32_t v = 0; v < RXD_WAVES; ++v)
+				all += s_w[v][t];
 			s_base[t] += all;
 		}
 		__syncthreads();
 	}
-	// counters (a slot short of packets shows in s_base > have below)
-	if (errs)
-		atomicAdd(&s_ctr[0], errs);
-	if (disc)
-		atomicAdd(&s_ctr[1], disc);
-	if (pkts)
-		atomicAdd(&s_ctr[2], pkts);
-	if (octs)
-		atomicAdd(&s_ctr[3], octs);
-	__syncthreads();
+	// counters: summed per wave (32-bit: at most 64 x 8 frames of 64 KiB),
+	// one LDS add per wave -- 1024 threads adding to one LDS word serialise
+	// (a slot short of packets shows in s_base > have below)
+	{
+		uint32_t v[4] = { errs, disc, pkts, octs };
+#pragma unroll
+		for (int j = 0; j < 4; ++j)
+#pragma unroll
+			for (int o = 32; o > 0; o >>= 1)
+				v[j] += (uint32_t)__shfl_xor((int)v[j], o);
+		if (lane == 0) {
+#pragma unroll
+			for (int j = 0; j < 4; ++j)
+				if (v[j])
+					atomicAdd(&s_ctr[j], v[j]);
+		}
+	}
+	if (group) {
+		// the stable permutation of the delivered frames by queue group
+		for (uint32_t i = t; i < n; i += RXD_THREADS)
+			if (s_q[i] < MI_CLS_DLV_GROUPS)
+				atomicAdd(&s_gcnt[s_q[i]], 1u);
+		__syncthreads();
+		if (t == 0) {
+			uint32_t at = 0;
+			for (uint32_t g = 0; g < MI_CLS_DLV_GROUPS; ++g) {
+				s_gpos[g] = at;
+				at += s_gcnt[g];
+			}
+		}
+		__syncthreads();
+#pragma unroll
+		for (uint32_t c = 0; c < RXD_PER; ++c) {
+			if (c >= nc)
+				continue;
+			const uint32_t i = c * RXD_THREADS + t;
+			const uint32_t q = i < n ? s_q[i] : 0xFFu;
+			bool left = q < MI_CLS_DLV_GROUPS;
+			uint32_t rank = 0;
+			if (lane < MI_CLS_DLV_GROUPS)
+				s_gw[wave][lane] = 0u;
+			for (;;) {
+				const unsigned long long m = __ballot(left);
+				if (!m)
+					break;
+				const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)q, (int)__builtin_ctzll(m));
+				const unsigned long long mv = __ballot(left && q == v);
+				if (left && q == v) {
+					rank = (uint32_t)__popcll(mv & lt);
+					left = false;
+				}
+				if (lane == 0)
+					s_gw[wave][v] = (uint32_t)__popcll(mv);
+			}
+			__syncthreads();
+			if (q < MI_CLS_DLV_GROUPS) {
+				uint32_t before = 0;
+				for (uint32_t v = 0; v < wave; ++v)
+					before += s_gw[v][q];
+				pos[c] = s_gpos[q] + before + rank;
+			}
+			__syncthreads();
+			if (t < MI_CLS_DLV_GROUPS) {
+				uint32_t all = 0;
+				for (uint32_t v = 0; v < RXD_WAVES; ++v)
+					all += s_gw[v][t];
+				s_gpos[t] += all;
+			}
+			__syncthreads();
+		}
+	} else {
+		__syncthreads();
+	}
+	// every output, after the last barrier
+#pragma unroll
+	for (uint32_t c = 0; c < RXD_PER; ++c) {
+		const uint32_t i = c * RXD_THREADS + t;
+		if (i >= n)
+			continue;
+		a.dec[i] = w[c];
+		d.dec[i] = w[c];
+		d.dq[i] = s_qh[qe[c]];
+		if (pos[c] != ~0u)
+			a.perm[pos[c]] = i;
+	}
+	if (group && t < MI_CLS_DLV_GROUPS)
+		a.gcnt[t] = s_gcnt[t];
 	if (t == 0) {
 		a.out->in_errors = s_ctr[0];
 		a.out->in_discards = s_ctr[1];
@@ -366,64 +488,11 @@ __global__ __launch_bounds__(RXD_THREADS) void mi_cls_rx_decide_kernel(mi_cls_rx
 		a.out->octets = s_ctr[3];
 		uint32_t sh = 0;
 		for (uint32_t k = 0; k < MI_CLS_RX_POOLS; ++k) {
-			a.out->used[k] = min(s_base[k], a.have[k]);
+			a.out->used[k] = min(s_base[k], s_have[k]);
 			a.out->need[k] = s_base[k];
-			sh |= s_base[k] > a.have[k] ? 1u : 0u;
+			sh |= s_base[k] > s_have[k] ? 1u : 0u;
 		}
 		a.out->short_pool = sh;
-	}
-	if (!group)
-		return;
-	// the stable permutation of the delivered frames by queue group
-	for (uint32_t i = t; i < a.n; i += RXD_THREADS)
-		if (s_q[i] < MI_CLS_DLV_GROUPS)
-			atomicAdd(&s_gcnt[s_q[i]], 1u);
-	__syncthreads();
-	if (t == 0) {
-		uint32_t at = 0;
-		for (uint32_t g = 0; g < MI_CLS_DLV_GROUPS; ++g) {
-			s_gpos[g] = at;
-			at += s_gcnt[g];
-		}
-	}
-	if (t < MI_CLS_DLV_GROUPS)
-		a.gcnt[t] = s_gcnt[t];
-	__syncthreads();
-	for (uint32_t c0 = 0; c0 < a.n; c0 += RXD_THREADS) {
-		const uint32_t i = c0 + t;
-		const uint32_t q = i < a.n ? s_q[i] : 0xFFu;
-		bool left = q < MI_CLS_DLV_GROUPS;
-		uint32_t rank = 0;
-		if (lane < MI_CLS_DLV_GROUPS)
-			s_gw[wave][lane] = 0u;
-		for (;;) {
-			const unsigned long long m = __ballot(left);
-			if (!m)
-				break;
-			const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)q, (int)__builtin_ctzll(m));
-			const unsigned long long mv = __ballot(left && q == v);
-			if (left && q == v) {
-				rank = (uint32_t)__popcll(mv & lt);
-				left = false;
-			}
-			if (lane == 0)
-				s_gw[wave][v] = (uint32_t)__popcll(mv);
-		}
-		__syncthreads();
-		if (q < MI_CLS_DLV_GROUPS) {
-			uint32_t before = 0;
-			for (uint32_t w = 0; w < wave; ++w)
-				before += s_gw[w][q];
-			a.perm[s_gpos[q] + before + rank] = i;
-		}
-		__syncthreads();
-		if (t < MI_CLS_DLV_GROUPS) {
-			uint32_t all = 0;
-			for (uint32_t w = 0; w < RXD_WAVES; ++w)
-				all += s_gw[w][t];
-			s_gpos[t] += all;
-		}
-		__syncthreads();
 	}
 }
 
@@ -432,23 +501,28 @@ __global__ __launch_bounds__(RXD_THREADS) void mi_cls_rx_decide_kernel(mi_cls_rx
 // mi_cls_deliver_kernel.  A fresh packet gets the whole line; a loop packet
 // received in its own buffer keeps its headroom and user pointer (read from
 // its line), and a pool switch takes the old packet's user pointer.
-__global__ __launch_bounds__(DLV_THREADS) void mi_cls_rx_deliver_kernel(mi_cls_rxc_args_t a)
+__global__ __launch_bounds__(DLV_THREADS) void mi_cls_rx_deliver_kernel(mi_cls_rxc_args_t a, mi_cls_rxdev_t d)
 {
 	const uint32_t sub = threadIdx.x & 15u;
 	const uint32_t i = blockIdx.x * DLV_PER_BLOCK + (threadIdx.x >> 4);
 	if (i >= a.n)
 		return;
-	const uint64_t e = a.ent[i];
+	// the frame's packet: the rank-th packet taken of its slot, or its own
+	const uint32_t dw = d.dec[i], fate = dw & 3u, k = (dw >> 2) & 31u, rank = dw >> 16;
+	const bool fresh = fate == MI_CLS_RXF_FRESH;
+	const uint64_t e = fresh ? (rank < a.have[k] ? a.got[a.got_base[k] + rank] : 0ull)
+				 : (fate == MI_CLS_RXF_INPLACE ? a.pk[i] : 0ull);
+	if (sub == 15u)
+		a.ent[i] = e;
+	if (sub == 14u)
+		a.res[i] = d.res[i];   // every frame's record, for the host
 	if (!e)
 		return;
-	const uint32_t fate = a.dec[i] & 3u;
-	const bool fresh = fate == MI_CLS_RXF_FRESH;
 	uint8_t *meta = (uint8_t *)(uintptr_t)(e + a.meta_off);
 	const uint32_t len = a.slen[i];
 	if (sub < 4u) {
-		const mi_cls_result_t r = a.res[i];
-		const mi_cls_rxtab_t &tab = *a.tab;
-		const uint64_t dq = tab.qh[tab.cos_q0[r.cos] + r.queue];
+		const mi_cls_result_t r = d.res[i];
+		const uint64_t dq = d.dq[i];
 		u32x4 v;
 		if (sub == 0u) {
 			const uint32_t doff = fresh ? a.headroom : ((const u32x4 *)meta)[0][0];
@@ -493,8 +567,54 @@ __global__ __launch_bounds__(DLV_THREADS) void mi_cls_rx_deliver_kernel(mi_cls_r
 	}
 }
 
+// Loop receive staging on the device (args.stage): each frame's descriptor
+// from its packet's header -- the data address (buffer + headroom) relative
+// to the burst's base, the length, the pool -- as the host's stage_frames
+// builds it for packets in page-locked pools.  A packet outside the
+// page-locked range gets an empty descriptor and sets not_in_place (the
+// host then stages and delivers the burst itself).
+__global__ __launch_bounds__(256) void mi_cls_rx_stage_kernel(mi_cls_rxc_args_t a, uint64_t bytes)
+{
+	// the page-locked flags go to LDS while the handles load (two host-link
+	// round trips per frame: the handle, then its header's words)
+	__shared__ uint8_t s_pin[64];
+	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	const uint8_t pin = a.tab->rt_pinned[threadIdx.x & 63u];
+	const uint64_t hp = a.pk[min(i, a.n - 1u)];
+	s_pin[threadIdx.x & 63u] = pin;
+	__syncthreads();
+	if (i >= a.n)
+		return;
+	const uint8_t *h = (const uint8_t *)(uintptr_t)hp;
+	const uint64_t head = *(const uint64_t *)(h + a.head_off);
+	const uint32_t pool = *(const uint16_t *)(h + a.pool_off);
+	const mi_cls_pkt_meta_t *m = (const mi_cls_pkt_meta_t *)(h + a.meta_off);
+	const uint64_t d = head + m->data_off, base = (uint64_t)(uintptr_t)a.base;
+	const uint32_t l = min(m->len, 65535u);
+	const bool ok = pool < 64u && s_pin[pool] && d >= base && d - base + l + 16u <= bytes;
+	((uint32_t *)a.soff)[i] = ok ? (uint32_t)(d - base) : 0u;
+	((uint16_t *)a.slen)[i] = ok ? (uint16_t)l : (uint16_t)0;
+	((uint8_t *)a.ppool)[i] = (uint8_t)(pool + 1u);
+	if (!ok)
+		a.out->not_in_place = 1u;
+}
+
+int mi_cls_launch_rx_stage(hipStream_t st, const mi_cls_rxc_args_t &a, uint64_t bytes, bool preload)
+{
+	if (preload) {
+		hipFuncAttributes fa;
+		return hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(&mi_cls_rx_stage_kernel)) ==
+		       hipSuccess ? 0 : -EIO;
+	}
+	mi_cls_rxc_args_t h = a;
+	uint64_t b = bytes;
+	void *args[] = { &h, &b };
+	return hipLaunchKernel(reinterpret_cast<const void *>(&mi_cls_rx_stage_kernel),
+			       dim3((a.n + 255u) / 256u), dim3(256), args, 0, st) == hipSuccess ? 0 : -EIO;
+}
+
 int mi_cls_launch_rx_chain(hipStream_t cls, hipStream_t dlv, hipEvent_t dep, const mi_cls_rxc_args_t &a,
-			   bool preload)
+			   const mi_cls_rxdev_t &d, bool preload)
 {
 	if (preload) {
 		hipFuncAttributes fa;
@@ -504,7 +624,8 @@ int mi_cls_launch_rx_chain(hipStream_t cls, hipStream_t dlv, hipEvent_t dep, con
 				       hipSuccess ? 0 : -EIO;
 	}
 	mi_cls_rxc_args_t h = a;
-	void *args[] = { &h };
+	mi_cls_rxdev_t hd = d;
+	void *args[] = { &h, &hd };
 	if (hipLaunchKernel(reinterpret_cast<const void *>(&mi_cls_rx_decide_kernel), dim3(1),
 			    dim3(RXD_THREADS), args, 0, cls) != hipSuccess ||
 	    hipEventRecord(dep, cls) != hipSuccess || hipStreamWaitEvent(dlv, dep, 0) != hipSuccess)

@@ -116,6 +116,7 @@ typedef struct {
 	/* receive chain (rxc_submit .. rxc_end): the burst classified, decided
 	 * and delivered by the GPU from one submission, `delivering` from it */
 	int chain;
+	int gstage;             /* loop burst staged by the GPU (only pk[] is set) */
 	int pk_pinned;          /* pk / ppool page-locked */
 	int rxc_pinned;         /* dec / cent / got / rxo page-locked */
 	uint32_t *dec;          /* per frame: decision word (MI_CLS_RXF_*, mi_cls.h) */
@@ -181,6 +182,8 @@ static int rx_finish(rt_pktio_t *e, rx_set_t *s, odp_packet_t out[], int max_out
 static int rx_dlv_end(rt_pktio_t *e, rx_set_t *s, odp_packet_t out[], int max_out);
 static rx_set_t *rx_age(rt_pktio_t *e, int k);
 static int stage_reserve(rx_set_t *s, uint32_t n, size_t bytes);
+static int rxc_loop_stage_ok(rt_pktio_t *e, rx_set_t *s, uint32_t max);
+static int loop_stage_hdrs(rt_pktio_t *e, rx_set_t *s, uint32_t n);
 
 static rt_pktio_t PK[RT_MAX_PKTIO];
 static odp_spinlock_t pk_lock;
@@ -1220,6 +1223,73 @@ static void cos_enq_run(odp_packet_t pk[], int num)
 	cos_vector_enq(dst, pk, num, cos, vpool, vmax);
 }
 
+/* The host's staging of n loop packets already in s->pk: lengths, pools,
+ * headrooms, user pointers and the descriptors.  Packets of page-locked
+ * pools are classified in place: the descriptors are their data addresses
+ * relative to the lowest pinned pool (one base for the burst; the GPU
+ * addresses that memory at the host's addresses).  A burst with a packet
+ * outside that range is copied into the stage instead.  0, or -1 when the
+ * stage cannot grow. */
+static int loop_stage_hdrs(rt_pktio_t *e, rx_set_t *s, uint32_t n)
+{
+	uint8_t *lo = NULL;
+	size_t span = 0, off = 0;
+	int in_place = s->arr_pinned && rt_pinned_arena(&lo, &span) && span < OOB_SPAN;
+	uint8_t pinned_of[RT_MAX_POOLS];
+
+	(void)e;
+	for (int k = 0; k < RT_MAX_POOLS; k++) {
+		rt_pool_t *rp = rt_pool((odp_pool_t)(uintptr_t)(k + 1));
+
+		pinned_of[k] = rp && rp->pinned;
+	}
+	/* header prefetch distance (ODP_AMD_LOOP_PF, A/B; 16 -> 96: loop receive
+	 * 17.5 -> 20.0 Mpkt/s, profiles/r04pf_loop_prefetch_ab.txt) */
+	static int pf = -1;
+
+	if (pf < 0)
+		pf = getenv("ODP_AMD_LOOP_PF") ? atoi(getenv("ODP_AMD_LOOP_PF")) : 96;
+	for (uint32_t i = 0; i < n; i++) {
+		if (i + pf < n) {   /* both header lines (the sender wrote them) */
+			const uint8_t *nh = (const uint8_t *)rt_pkt_hdr(s->pk[i + pf]);
+
+			__builtin_prefetch(nh);
+			__builtin_prefetch(nh + 64);
+		}
+		pkt_hdr_t *h = rt_pkt_hdr(s->pk[i]);
+		const uint8_t *d = h->head + h->data_off;
+		uint32_t l = h->len > 65535 ? 65535 : h->len;
+		const uint32_t pi = h->ev.pool;
+
+		s->slen[i] = (uint16_t)l;
+		s->ppool[i] = (uint8_t)(pi + 1u);
+		s->pdoff[i] = (uint16_t)h->data_off;
+		s->pup[i] = h->user_ptr;
+		if (in_place && pinned_of[pi] && d >= lo && (size_t)(d - lo) + l + 16u <= span)
+			s->soff[i] = (uint32_t)(d - lo);
+		else
+			in_place = 0;
+	}
+	if (in_place) {
+		s->base = lo;
+		s->bytes = span;
+		return 0;
+	}
+	for (uint32_t i = 0; i < n; i++) {
+		pkt_hdr_t *h = rt_pkt_hdr(s->pk[i]);
+		const uint32_t l = s->slen[i];
+
+		if (stage_reserve(s, n, off + l + 64))
+			return -1;
+		memcpy(s->stage + off, h->head + h->data_off, l);
+		s->soff[i] = (uint32_t)off;
+		off += (l + 63u) & ~63u;
+	}
+	s->base = s->stage;
+	s->bytes = off + 64;
+	return 0;
+}
+
 /* Pull up to `max` frames from the driver into staging set s.  pcap frames
  * in a page-locked frame store are not copied: the set points at the store
  * (the GPU reads them there) and they are copied once, into their packets,
@@ -1274,28 +1344,10 @@ static int stage_frames(rt_pktio_t *e, rx_set_t *s, uint32_t max)
 		}
 		s->bytes = in_place ? e->fbuf_bytes : off + 64;
 	} else if (e->drv == DRV_LOOP) {
-		/* Packets of page-locked pools are classified in place: the
-		 * descriptors are their data addresses relative to the lowest
-		 * pinned pool (one base for the burst; the GPU addresses that
-		 * memory at the host's addresses).  A burst with a packet outside
-		 * that range is copied into the stage instead. */
-		uint8_t *lo = NULL;
-		size_t span = 0;
-		int in_place = s->arr_pinned && rt_pinned_arena(&lo, &span) && span < OOB_SPAN;
-		uint8_t pinned_of[RT_MAX_POOLS];
+		/* the receive chain stages the burst on the GPU from the packets'
+		 * headers (rxc_submit): only the handles are taken here */
+		const int gstage = rxc_loop_stage_ok(e, s, max);
 
-		for (int k = 0; k < RT_MAX_POOLS; k++) {
-			rt_pool_t *rp = rt_pool((odp_pool_t)(uintptr_t)(k + 1));
-
-			pinned_of[k] = rp && rp->pinned;
-		}
-
-		/* header prefetch distance (ODP_AMD_LOOP_PF, A/B; 16 -> 96: loop receive
-		 * 17.5 -> 20.0 Mpkt/s, profiles/r04pf_loop_prefetch_ab.txt) */
-		static int pf = -1;
-
-		if (pf < 0)
-			pf = getenv("ODP_AMD_LOOP_PF") ? atoi(getenv("ODP_AMD_LOOP_PF")) : 96;
 		while (n < max) {
 			odp_event_t *ev = (odp_event_t *)(void *)(s->pk + n);
 			int want = (int)(max - n);
@@ -1303,51 +1355,23 @@ static int stage_frames(rt_pktio_t *e, rx_set_t *s, uint32_t max)
 
 			if (got <= 0)
 				break;
-			for (int i = 0; i < got; i++) {
-				if (i + pf < got) {   /* both header lines (the sender wrote them) */
-					const uint8_t *nh = (const uint8_t *)rt_pkt_hdr(odp_packet_from_event(ev[i + pf]));
-
-					__builtin_prefetch(nh);
-					__builtin_prefetch(nh + 64);
-				}
-				odp_packet_t p = odp_packet_from_event(ev[i]);
-				pkt_hdr_t *h = rt_pkt_hdr(p);
-				const uint8_t *d = h->head + h->data_off;
-				uint32_t l = h->len > 65535 ? 65535 : h->len;
-				const uint32_t pi = h->ev.pool;
-
-				s->pk[n] = p;
-				s->slen[n] = (uint16_t)l;
-				s->ppool[n] = (uint8_t)(pi + 1u);
-				s->pdoff[n] = (uint16_t)h->data_off;
-				s->pup[n] = h->user_ptr;
-				if (in_place && pinned_of[pi] && d >= lo && (size_t)(d - lo) + l + 16u <= span)
-					s->soff[n] = (uint32_t)(d - lo);
-				else
-					in_place = 0;
-				n++;
-			}
+			n += (uint32_t)got;
 			if (got < want)
 				break;
 		}
-		if (in_place) {
+		/* the GPU reads the headers: only of packets in page-locked pools
+		 * (a packet of a pool in ordinary memory is staged by the host) */
+		s->gstage = gstage && n > 0 && rt_pinned_handles(s->pk, (int)n);
+		if (s->gstage) {
+			uint8_t *lo = NULL;
+			size_t span = 0;
+
+			(void)rt_pinned_arena(&lo, &span);
 			s->base = lo;
 			s->bytes = span;
-		} else {
-			for (uint32_t i = 0; i < n; i++) {
-				pkt_hdr_t *h = rt_pkt_hdr(s->pk[i]);
-				const uint32_t l = s->slen[i];
-
-				if (stage_reserve(s, max, off + l + 64)) {
-					odp_packet_free_multi(s->pk, (int)n);
-					return -1;
-				}
-				memcpy(s->stage + off, h->head + h->data_off, l);
-				s->soff[i] = (uint32_t)off;
-				off += (l + 63u) & ~63u;
-			}
-			s->base = s->stage;
-			s->bytes = off + 64;
+		} else if (n > 0 && loop_stage_hdrs(e, s, n)) {
+			odp_packet_free_multi(s->pk, (int)n);
+			return -1;
 		}
 	}
 	return (int)n;
@@ -2474,6 +2498,11 @@ static int rxc_table(rt_pktio_t *e)
 			e->rxtab->rt_slot[idx] = (uint8_t)(k + 1u);
 		}
 	}
+	for (int k = 0; ok && k < RT_MAX_POOLS && k < 64; k++) {
+		rt_pool_t *rp = rt_pool((odp_pool_t)(uintptr_t)(k + 1));
+
+		e->rxtab->rt_pinned[k] = rp && rp->pinned;
+	}
 	if (e->rx_np != np)
 		memset(e->rx_want, 0, sizeof(e->rx_want));   /* first bursts: as many as frames */
 	e->rx_np = np;
@@ -2484,6 +2513,33 @@ static int rxc_table(rt_pktio_t *e)
 
 /* Submit set s's burst as a chain: 1, or 0 when it takes the other path
  * (nothing done then). */
+/* Whether this pktio's loop bursts can be staged by the GPU (the chain's
+ * conditions, and an arena of page-locked pools to address them in). */
+static int rxc_loop_stage_ok(rt_pktio_t *e, rx_set_t *s, uint32_t max)
+{
+	uint8_t *lo = NULL;
+	size_t span = 0;
+
+	return rx_chain_on() && gpu_deliver_on() && e->cls_enabled && e->parse_layer == ODP_PROTO_LAYER_ALL &&
+	       s->rxc_pinned && s->dlv_pinned && s->arr_pinned && s->pk_pinned && max > 0 &&
+	       max <= MI_CLS_DLV_GROUP_MAX && rt_pinned_arena(&lo, &span) && span < OOB_SPAN &&
+	       rxc_table(e) == 0;
+}
+
+/* A burst that does not take the chain: a loop burst left for the GPU to
+ * stage is staged by the host now (the classic path reads its descriptors). */
+static int rxc_no(rt_pktio_t *e, rx_set_t *s)
+{
+	if (s->gstage) {
+		s->gstage = 0;
+		if (loop_stage_hdrs(e, s, (uint32_t)s->n)) {
+			rx_drop(e, s, -ENOMEM);
+			s->n = 0;
+		}
+	}
+	return 0;
+}
+
 static int rxc_submit(rt_pktio_t *e, rx_set_t *s)
 {
 	const uint32_t n = (uint32_t)s->n;
@@ -2491,7 +2547,7 @@ static int rxc_submit(rt_pktio_t *e, rx_set_t *s)
 	if (!rx_chain_on() || !gpu_deliver_on() || !e->cls_enabled || e->parse_layer != ODP_PROTO_LAYER_ALL ||
 	    !s->rxc_pinned || !s->dlv_pinned || !s->arr_pinned || n == 0 || n > MI_CLS_DLV_GROUP_MAX ||
 	    (e->drv == DRV_LOOP && !s->pk_pinned) || !mi_cls_host_mapped(s->base) || rxc_table(e))
-		return 0;
+		return rxc_no(e, s);
 	/* the packets of each pool slot, in the order the frames take them */
 	uint32_t at = 0;
 
@@ -2527,10 +2583,27 @@ static int rxc_submit(rt_pktio_t *e, rx_set_t *s)
 	memcpy(a.got_base, s->cbase, sizeof(a.got_base));
 	memcpy(a.have, s->chave, sizeof(a.have));
 	if (e->drv == DRV_LOOP) {
+		/* the GPU reads the loop packets' metadata (a pool switch takes the
+		 * old packet's user pointer): every packet in a page-locked pool
+		 * (checked by address for a GPU-staged burst, by pool here) */
+		if (!s->gstage)
+			for (uint32_t i = 0; i < n; i++)
+				if (!s->ppool[i] || !e->rxtab->rt_pinned[(s->ppool[i] - 1u) & 63u]) {
+					for (uint32_t k = 0; k < s->cnp; k++)
+						rt_packet_return_raw(s->cpool[k],
+								     (const odp_packet_t *)(const void *)(s->got +
+													   s->cbase[k]),
+								     (int)s->chave[k]);
+					return rxc_no(e, s);
+				}
 		a.pk = (const uint64_t *)(const void *)s->pk;
 		a.ppool = s->ppool;
+		a.stage = (uint32_t)s->gstage;
+		a.head_off = (uint16_t)__builtin_offsetof(pkt_hdr_t, head);
+		a.pool_off = (uint16_t)__builtin_offsetof(pkt_hdr_t, ev.pool);
 	}
 	a.meta_off = (uint32_t)__builtin_offsetof(pkt_hdr_t, meta);
+	s->rxo->not_in_place = 0;
 	a.dec = s->dec;
 	a.ent = s->cent;
 	a.perm = s->perm;
@@ -2544,7 +2617,7 @@ static int rxc_submit(rt_pktio_t *e, rx_set_t *s)
 			rt_packet_return_raw(s->cpool[k], (const odp_packet_t *)(const void *)(s->got + s->cbase[k]),
 					     (int)s->chave[k]);
 		s->dticket = 0;
-		return 0;
+		return rxc_no(e, s);
 	}
 	s->chain = 1;
 	s->ticket = 0;
@@ -2575,20 +2648,30 @@ static int rxc_end(rt_pktio_t *e, rx_set_t *s, odp_packet_t out[], int max_out)
 		for (uint32_t k = 0; k < s->cnp && k < e->rx_np; k++)
 			e->rx_want[k] = o->need[k] + o->need[k] / 4u + 32u;
 	}
-	if (rc || o->short_pool || s->dgen != odp_amd_cls_generation()) {
+	if (rc || o->short_pool || o->not_in_place || s->dgen != odp_amd_cls_generation()) {
 		/* every packet taken for the burst back; the host path then
 		 * decides, allocates and delivers from the records (the classify
-		 * records are valid; a control-plane change re-classifies) */
+		 * records are valid; a control-plane change re-classifies).  A loop
+		 * burst the GPU staged is staged and classified again by the host
+		 * (its headrooms and user pointers are the host path's inputs; a
+		 * packet outside the page-locked arena is copied) */
 		for (uint32_t k = 0; k < s->cnp; k++)
 			rt_packet_return_raw(s->cpool[k], (const odp_packet_t *)(const void *)(s->got + s->cbase[k]),
 					     (int)s->chave[k]);
 		if (rc) {
+			s->gstage = 0;
 			rx_drop(e, s, rc);
 			return 0;
+		}
+		if (s->gstage) {
+			s->gstage = 0;
+			if (loop_stage_hdrs(e, s, (uint32_t)s->n) || rx_classify(e, s, 0))
+				return 0;   /* dropped and counted */
 		}
 		s->pending = 1;
 		return rx_finish(e, s, out, max_out);
 	}
+	s->gstage = 0;
 	const uint64_t tk1 = prof_ns();
 
 	for (uint32_t k = 0; k < s->cnp; k++)

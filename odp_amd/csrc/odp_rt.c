@@ -535,6 +535,39 @@ static int pool_pageable(const char *name)
 	return 0;
 }
 
+/* 1 when every packet handle of pk[0..n) is a header inside a page-locked
+ * pool's memory (the GPU may then read it), else 0.  Only the handles are
+ * compared against the pools' address ranges: no header is read. */
+int rt_pinned_handles(const odp_packet_t pk[], int n)
+{
+	uintptr_t lo[RT_MAX_POOLS], hi[RT_MAX_POOLS];
+	int np = 0, last = 0;
+
+	for (int i = 0; i < RT_MAX_POOLS; i++) {
+		const rt_pool_t *p = &RT.pool[i];
+
+		if (p->used && p->pinned && p->mem) {
+			lo[np] = (uintptr_t)p->mem;
+			hi[np] = (uintptr_t)p->mem + p->elem_size * p->num;
+			np++;
+		}
+	}
+	for (int i = 0; i < n; i++) {
+		const uintptr_t a = (uintptr_t)pk[i];
+
+		if (np && a >= lo[last] && a + sizeof(pkt_hdr_t) <= hi[last])
+			continue;
+		int k = 0;
+
+		while (k < np && !(a >= lo[k] && a + sizeof(pkt_hdr_t) <= hi[k]))
+			k++;
+		if (k == np)
+			return 0;
+		last = k;
+	}
+	return 1;
+}
+
 int rt_pinned_arena(uint8_t **lo, size_t *bytes)
 {
 	uint8_t *a = NULL, *b = NULL;

@@ -149,6 +149,9 @@ int rt_queue_is_valid(odp_queue_t h);
 /* the address range spanned by the pinned packet pools ([*lo, *lo + *bytes));
  * 0 when there is none */
 int rt_pinned_arena(uint8_t **lo, size_t *bytes);
+/* 1 when every handle of pk[0..n) is a header in a page-locked pool (the
+ * GPU may read it): the handles' addresses against the pools' ranges */
+int rt_pinned_handles(const odp_packet_t pk[], int n);
 /* bytes from a packet header's metadata block to its data at the default
  * headroom (fixed by the pool layout) */
 uint32_t rt_data_from_meta(void);

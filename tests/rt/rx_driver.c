@@ -416,7 +416,12 @@ int main(int argc, char *argv[])
 	int rounds = getenv("RX_LOOP_ROUNDS") ? atoi(getenv("RX_LOOP_ROUNDS")) : 1;
 	uint64_t timed_ns = 0;
 
-	if (is_loop && feed_loop(argv[7], pool, pktio) < 0)
+	/* RX_FEED_POOL=1: the loop "wire" sends packets of a pool of its own
+	 * ("feedPool"; with ODP_AMD_PAGEABLE_POOLS=feedPool in ordinary memory,
+	 * outside the page-locked arena the GPU stages loop packets in) */
+	odp_pool_t feed_pool = getenv("RX_FEED_POOL") ? mkpool("feedPool") : pool;
+
+	if (is_loop && feed_loop(argv[7], feed_pool, pktio) < 0)
 		return 9;
 	if (is_loop && rounds > 1)
 		t_start = odp_time_local();
@@ -479,7 +484,7 @@ again:
 		}
 		if (is_loop && --rounds > 0) {
 			timed_ns += odp_time_diff_ns(odp_time_local(), t_start);
-			if (feed_loop(argv[7], pool, pktio) < 0)
+			if (feed_loop(argv[7], feed_pool, pktio) < 0)
 				return 9;
 			t_start = odp_time_local();
 			goto again;

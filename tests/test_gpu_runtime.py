@@ -318,3 +318,32 @@ def test_rx_burst_above_device_grouping(built, gpu, tmp_path):
     frames = [b.frame(i) for i in range(b.n)]
     got = _run_case(tmp_path, prog, frames, mode="direct", burst=9000)
     assert sum(len(v) for v in got[0].values()) == 20000
+
+
+def test_rx_chain_short_pool_redo(built, gpu, tmp_path):
+    """The receive chain takes each burst's packets from the CoS pools before
+    the GPU decides (as many per pool as the previous bursts needed, plus a
+    margin).  Traffic whose CoS mix flips between bursts leaves a pool short:
+    that burst is delivered again by the host path, and every queue's packets,
+    order, pools and counters stay the reference's."""
+    from odp_amd import pktgen as pg
+    prog = [R.cos("default", queue=1), R.cos("a", queue=2), R.cos("b", queue=3), ("default", 0),
+            ("pmr", [R.t_be16(R.PMR_UDP_DPORT, 1111)], 0, 1, 5),
+            ("pmr", [R.t_be16(R.PMR_UDP_DPORT, 2222)], 0, 2, 6)]
+    frames = []
+    for blk in range(12):
+        port = 1111 if blk % 3 == 0 else (2222 if blk % 3 == 1 else 3333)
+        frames += [pg.udp4_frame(src=f"10.1.{blk}.{i % 250}", dport=port, size=60 + (i % 5) * 40)
+                   for i in range(64)]
+    frames = H.pcap_frames(frames)
+    _run_case(tmp_path, prog, frames, mode="direct", cos_pools=1, burst=64)
+
+
+def test_rx_loop_packets_outside_pinned_arena(built, gpu, tmp_path):
+    """Loop packets from a pool in ordinary memory: the GPU staging of the
+    loop burst finds them outside the page-locked arena (not_in_place) and
+    the host stages (copies), classifies and delivers that burst; the result
+    is the reference's."""
+    frames = H.pcap_frames([f for _, f in zoo.all_frames()])
+    _run_case(tmp_path, zoo.prog_everything(), frames, pktio="loop", cos_pools=0, burst=32,
+              env_extra={"RX_FEED_POOL": "1", "ODP_AMD_PAGEABLE_POOLS": "feedPool"})
