@@ -417,6 +417,8 @@ typedef struct mi_cls_rxtab {
 	uint8_t  rt_pinned[64];       /* runtime pool index -> 1: page-locked pool   */
 	uint64_t qh[MI_CLS_RX_QENT];  /* odp_queue_t per (CoS, queue slot)          */
 	uint8_t  qg[MI_CLS_RX_QENT];  /* its queue group 0..63 (MI_CLS_RXT_GROUP)   */
+	uint64_t stamp;               /* new value whenever the table is rewritten: */
+				      /* the device keeps a copy per stamp          */
 } mi_cls_rxtab_t;
 
 typedef struct mi_cls_rx_out {

@@ -2911,9 +2911,8 @@ int mi_cls_launch_ck(int nw, bool lt, bool div, unsigned grid, size_t dyn, hipSt
 		     const KArgs &a);
 // receive delivery (mi_cls_kd.hip); grid 0: preload only
 int mi_cls_launch_deliver(unsigned grid, hipStream_t st, const mi_cls_dlv_args_t &h);
-// receive chain (mi_cls_kd.hip): decisions on `cls` after the burst's
-// classification, `dep` recorded there, the delivery on `dlv` after it;
-// preload: resolve both kernels only.  The chain's device-resident
+// receive chain (mi_cls_kd.hip): the decisions, then the delivery, on `st`
+// after the burst's classification; preload: resolve both kernels only.  The chain's device-resident
 // per-burst arrays (the context's, one set per ticket slot): the records
 // (the classification writes them here; the delivery copies them to
 // args.res), the decision words and each enqueued frame's queue handle --
@@ -2923,11 +2922,15 @@ struct mi_cls_rxdev_t {
 	mi_cls_result_t *res;
 	uint32_t *dec;
 	uint64_t *dq;
+	uint16_t *len;              // dlen: each frame's length, and
+	uint8_t *pp;                //       its packet's pool + 1 (the stage kernel's)
+	const mi_cls_rxtab_t *tab;  // the table's copy in HBM
+	uint32_t dlen;              // 1: len / pp hold the burst (else args.slen / ppool)
 };
-int mi_cls_launch_rx_chain(hipStream_t cls, hipStream_t dlv, hipEvent_t dep, const mi_cls_rxc_args_t &a,
-			   const mi_cls_rxdev_t &d, bool preload);
+int mi_cls_launch_rx_chain(hipStream_t st, const mi_cls_rxc_args_t &a, const mi_cls_rxdev_t &d, bool preload);
 // loop receive staging on the device (mi_cls_rxc_args_t.stage)
-int mi_cls_launch_rx_stage(hipStream_t st, const mi_cls_rxc_args_t &a, uint64_t bytes, bool preload);
+int mi_cls_launch_rx_stage(hipStream_t st, const mi_cls_rxc_args_t &a, const mi_cls_rxdev_t &d, uint64_t bytes,
+			   bool preload);
 
 // Every launcher goes through mi_launch.  grid == 0 launches nothing: it
 // resolves the instantiation on the current device (hipFuncGetAttributes

@@ -252,22 +252,29 @@ int mi_cls_launch_deliver(unsigned grid, hipStream_t st, const mi_cls_dlv_args_t
 // Decisions of frames [0, n) in arrival order: fate, pool slot, the frame's
 // rank among its slot's frames (which packet of the slot it takes), queue
 // group; the pktio counters; the stable grouping by queue (as dlv_group);
-// `short_pool` when a slot has too few packets.  One block.  Latency rules
-// it, not bytes: every load of the inputs (records in HBM; lengths, pools and
-// the table in host memory) is issued before any is used, each thread's
-// frames stay in registers (fully unrolled, constant indexes: nothing in
-// scratch), and every store goes out after the last barrier -- a barrier
-// waits for the block's outstanding stores, which to host memory are a
-// host-link round trip each (the first version's 26 barriers behind host
-// stores took 84 us per 4096-frame burst).
+// `short_pool` when a slot has too few packets.  One block of 16 waves.
+// Latency rules it, not bytes:
+//  - every load of the inputs (records in HBM; lengths, pools and the table
+//    in host memory) is issued before any is used, and each thread's frames
+//    stay in registers (fully unrolled, constant indexes: nothing in scratch);
+//  - the ranks are scans over LDS, one wave per pool slot (16) and per four
+//    queue groups (64): a ballot per 64 frames, so 5 barriers per burst, not
+//    3 per 1024 frames and a ballot per distinct value;
+//  - every store goes out after the last barrier: a barrier waits for the
+//    block's outstanding stores, which to host memory take a host-link round
+//    trip each.
 #define RXD_PER 8   // frames per thread (MI_CLS_DLV_GROUP_MAX / RXD_THREADS)
+#define RXD_SEG 8   // 64-frame segments per batch of LDS reads in the scans
 static_assert(RXD_PER * RXD_THREADS == MI_CLS_DLV_GROUP_MAX, "one block holds a burst");
+static_assert(RXD_WAVES == MI_CLS_RX_POOLS, "one wave per pool slot");
+static_assert(RXD_WAVES * 4 == MI_CLS_DLV_GROUPS, "four queue groups per wave");
 __global__ __launch_bounds__(RXD_THREADS) void mi_cls_rx_decide_kernel(mi_cls_rxc_args_t a, mi_cls_rxdev_t d)
 {
-	__shared__ uint8_t s_q[MI_CLS_DLV_GROUP_MAX];
-	__shared__ uint32_t s_w[RXD_WAVES][MI_CLS_RX_POOLS];   // per wave: fresh frames per slot
-	__shared__ uint32_t s_base[MI_CLS_RX_POOLS];           // frames of each slot so far
-	__shared__ uint32_t s_gw[RXD_WAVES][MI_CLS_DLV_GROUPS];
+	__shared__ uint8_t s_k[MI_CLS_DLV_GROUP_MAX];        // fresh frame: its slot, else 0xFF
+	__shared__ uint8_t s_q[MI_CLS_DLV_GROUP_MAX];        // its queue group, else 0xFF
+	__shared__ uint16_t s_rank[MI_CLS_DLV_GROUP_MAX];    // fresh frame: rank in its slot
+	__shared__ uint16_t s_perm[MI_CLS_DLV_GROUP_MAX];
+	__shared__ uint32_t s_need[MI_CLS_RX_POOLS];
 	__shared__ uint32_t s_gcnt[MI_CLS_DLV_GROUPS], s_gpos[MI_CLS_DLV_GROUPS];
 	__shared__ uint32_t s_ctr[4];
 	__shared__ uint8_t s_cpool[256], s_rts[64], s_qg[MI_CLS_RX_QENT];
@@ -275,21 +282,26 @@ __global__ __launch_bounds__(RXD_THREADS) void mi_cls_rx_decide_kernel(mi_cls_rx
 	__shared__ uint64_t s_qh[MI_CLS_RX_QENT];
 	__shared__ uint32_t s_cap[MI_CLS_RX_POOLS], s_have[MI_CLS_RX_POOLS];
 	const uint32_t t = threadIdx.x, lane = t & (WAVE - 1), wave = t / WAVE;
-	const mi_cls_rxtab_t &tab = *a.tab;
+	const mi_cls_rxtab_t &tab = *d.tab;
 	const bool group = (tab.flags & MI_CLS_RXT_GROUP) != 0u;
 	const unsigned long long lt = lane ? (~0ull >> (64u - lane)) : 0ull;
-	const uint32_t n = a.n, nc = (n + RXD_THREADS - 1u) / RXD_THREADS;
+	const uint32_t n = a.n, nseg = (n + WAVE - 1u) / WAVE;
 	// this thread's frames t, t + 1024, ..: unconditional loads (indexes
 	// clamped into the burst, a valid byte array when there is no ppool), so
-	// no branch makes the compiler wait for one before the next is issued
+	// no branch makes the compiler wait for one before the next is issued.
+	// The records and the table are in HBM, and so are the lengths and pools
+	// of a burst the stage kernel staged: a GPU-staged burst reads nothing
+	// over the host link here (reads there queue behind the other burst's
+	// delivery traffic)
 	mi_cls_result_t r[RXD_PER];
 	uint32_t len[RXD_PER], pp[RXD_PER];
-	const uint8_t *ppa = a.pk ? a.ppool : (const uint8_t *)a.slen;
+	const uint16_t *lena = d.dlen ? d.len : a.slen;
+	const uint8_t *ppa = a.pk ? (d.dlen ? d.pp : a.ppool) : (const uint8_t *)lena;
 #pragma unroll
 	for (uint32_t c = 0; c < RXD_PER; ++c) {
 		const uint32_t i = min(c * RXD_THREADS + t, n - 1u);
 		r[c] = d.res[i];
-		len[c] = a.slen[i];
+		len[c] = lena[i];
 		pp[c] = ppa[i];
 	}
 	// the table's words, also unconditional (wrapped indexes); every thread
@@ -309,20 +321,14 @@ __global__ __launch_bounds__(RXD_THREADS) void mi_cls_rx_decide_kernel(mi_cls_rx
 		s_rts[t & 63u] = rs;
 		s_cap[t & (MI_CLS_RX_POOLS - 1u)] = cap;
 		s_have[t & (MI_CLS_RX_POOLS - 1u)] = hv;
-		s_base[t & (MI_CLS_RX_POOLS - 1u)] = 0u;
-		s_gcnt[t & (MI_CLS_DLV_GROUPS - 1u)] = 0u;
 		s_ctr[t & 3u] = 0u;
 	}
 	__syncthreads();
-	uint32_t w[RXD_PER], qe[RXD_PER], pos[RXD_PER];
-	uint32_t errs = 0, disc = 0, pkts = 0, octs = 0;
+	// (1) each frame's fate and slot (odp_packet_io.c:680-705 per frame)
+	uint32_t fk[RXD_PER], qe[RXD_PER];
+	uint32_t errs = 0, disc = 0;
 #pragma unroll
 	for (uint32_t c = 0; c < RXD_PER; ++c) {
-		w[c] = 0u;
-		qe[c] = 0u;
-		pos[c] = ~0u;
-		if (c >= nc)   // uniform
-			continue;
 		const uint32_t i = c * RXD_THREADS + t;
 		const bool in = i < n;
 		const uint32_t p = a.pk ? pp[c] : 0u;
@@ -332,71 +338,68 @@ __global__ __launch_bounds__(RXD_THREADS) void mi_cls_rx_decide_kernel(mi_cls_rx
 			if (r[c].outcome == MI_CLS_OUT_DISCARD || r[c].outcome == MI_CLS_OUT_LOOP) {
 				fate = MI_CLS_RXF_DISCARD;
 			} else if (r[c].outcome == MI_CLS_OUT_ENQ) {
-				k = s_cpool[r[c].cos];
+				k = s_cpool[r[c].cos] & (MI_CLS_RX_POOLS - 1u);
 				const uint32_t own = p ? s_rts[(p - 1u) & 63u] : 0u;
 				if (own != 0u && own - 1u == k)
 					fate = MI_CLS_RXF_INPLACE;
-				else if (len[c] > s_cap[k & (MI_CLS_RX_POOLS - 1u)])
+				else if (len[c] > s_cap[k])
 					fate = MI_CLS_RXF_DISCARD;   // odp_packet_alloc fails
 				else
 					fate = MI_CLS_RXF_FRESH;
 			}
+			s_k[i] = fate == MI_CLS_RXF_FRESH ? (uint8_t)k : (uint8_t)0xFFu;
 		}
-		k &= MI_CLS_RX_POOLS - 1u;
-		// rank among the slot's fresh frames: the wave's lanes before this
-		// one (a ballot per slot present in the wave), then the earlier
-		// waves of the chunk and the earlier chunks
-		const bool fr = fate == MI_CLS_RXF_FRESH;
-		uint32_t rank = 0;
-		if (lane < MI_CLS_RX_POOLS)
-			s_w[wave][lane] = 0u;
-		{
-			bool left = fr;
-			for (;;) {
-				const unsigned long long m = __ballot(left);
-				if (!m)
-					break;
-				const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)k, (int)__builtin_ctzll(m));
-				const unsigned long long mv = __ballot(left && k == v);
-				if (left && k == v) {
-					rank = (uint32_t)__popcll(mv & lt);
-					left = false;
-				}
-				if (lane == 0)
-					s_w[wave][v] = (uint32_t)__popcll(mv);
+		disc += fate == MI_CLS_RXF_DISCARD ? 1u : 0u;
+		fk[c] = fate | (k << 2);
+		qe[c] = min(in && r[c].outcome == MI_CLS_OUT_ENQ ? s_q0[r[c].cos] + r[c].queue : 0u,
+			    (uint32_t)MI_CLS_RX_QENT - 1u);
+	}
+	__syncthreads();
+	// (2) wave k ranks slot k's fresh frames in arrival order (the LDS
+	// reads of 8 segments issued together: one read's latency per 8)
+	{
+		uint32_t base = 0;
+		for (uint32_t g0 = 0; g0 < nseg; g0 += RXD_SEG) {
+			uint32_t v[RXD_SEG];
+#pragma unroll
+			for (uint32_t j = 0; j < RXD_SEG; ++j) {
+				const uint32_t i = (g0 + j) * WAVE + lane;
+				v[j] = i < n ? s_k[i] : 0xFFu;
+			}
+#pragma unroll
+			for (uint32_t j = 0; j < RXD_SEG; ++j) {
+				const uint32_t i = (g0 + j) * WAVE + lane;
+				const bool mine = v[j] == wave;
+				const unsigned long long m = __ballot(mine);
+				if (mine)
+					s_rank[i] = (uint16_t)min(base + (uint32_t)__popcll(m & lt), 0xFFFFu);
+				base += (uint32_t)__popcll(m);
 			}
 		}
-		__syncthreads();
-		if (fr) {
-			for (uint32_t v = 0; v < wave; ++v)
-				rank += s_w[v][k];
-			rank += s_base[k];
-		}
-		const bool dlv = (fr && rank < s_have[k]) || fate == MI_CLS_RXF_INPLACE;
-		if (fate == MI_CLS_RXF_DISCARD)
-			++disc;
+		if (lane == 0)
+			s_need[wave] = base;
+	}
+	__syncthreads();
+	// (3) delivered or not, the counters, the queue group
+	uint32_t w[RXD_PER];
+	uint32_t pkts = 0, octs = 0;
+#pragma unroll
+	for (uint32_t c = 0; c < RXD_PER; ++c) {
+		const uint32_t i = c * RXD_THREADS + t;
+		const uint32_t fate = fk[c] & 3u, k = fk[c] >> 2;
+		const uint32_t rank = fate == MI_CLS_RXF_FRESH ? s_rank[min(i, n - 1u)] : 0u;
+		const bool dlv = (fate == MI_CLS_RXF_FRESH && rank < s_have[k]) || fate == MI_CLS_RXF_INPLACE;
 		if (dlv && r[c].err == 0u) {
 			++pkts;
 			octs += len[c];
 		}
-		qe[c] = min(in && r[c].outcome == MI_CLS_OUT_ENQ ? s_q0[r[c].cos] + r[c].queue : 0u,
-			    (uint32_t)MI_CLS_RX_QENT - 1u);
 		const uint32_t qid = dlv && group ? s_qg[qe[c]] : 0x7Fu;
-		w[c] = fate | (k << 2) | ((qid & 0x7Fu) << 8) | (min(rank, 0xFFFFu) << 16);
-		if (in)
+		w[c] = fk[c] | ((qid & 0x7Fu) << 8) | (rank << 16);
+		if (i < n)
 			s_q[i] = (uint8_t)(qid < MI_CLS_DLV_GROUPS ? qid : 0xFFu);
-		__syncthreads();
-		if (t < MI_CLS_RX_POOLS) {
-			uint32_t all = 0;
-			for (uint32_t v = 0; v < RXD_WAVES; ++v)
-				all += s_w[v][t];
-			s_base[t] += all;
-		}
-		__syncthreads();
 	}
 	// counters: summed per wave (32-bit: at most 64 x 8 frames of 64 KiB),
-	// one LDS add per wave -- 1024 threads adding to one LDS word serialise
-	// (a slot short of packets shows in s_base > have below)
+	// one LDS add per wave
 	{
 		uint32_t v[4] = { errs, disc, pkts, octs };
 #pragma unroll
@@ -411,60 +414,61 @@ __global__ __launch_bounds__(RXD_THREADS) void mi_cls_rx_decide_kernel(mi_cls_rx
 					atomicAdd(&s_ctr[j], v[j]);
 		}
 	}
+	__syncthreads();
+	// (4) the stable permutation of the delivered frames by queue group:
+	// wave w counts, then places, groups 4w .. 4w + 3
+	uint32_t ngrp = 0;
 	if (group) {
-		// the stable permutation of the delivered frames by queue group
-		for (uint32_t i = t; i < n; i += RXD_THREADS)
-			if (s_q[i] < MI_CLS_DLV_GROUPS)
-				atomicAdd(&s_gcnt[s_q[i]], 1u);
-		__syncthreads();
-		if (t == 0) {
-			uint32_t at = 0;
-			for (uint32_t g = 0; g < MI_CLS_DLV_GROUPS; ++g) {
-				s_gpos[g] = at;
-				at += s_gcnt[g];
-			}
-		}
-		__syncthreads();
+		uint32_t cnt[4] = { 0u, 0u, 0u, 0u };
+		for (uint32_t g0 = 0; g0 < nseg; g0 += RXD_SEG) {
+			uint32_t v[RXD_SEG];
 #pragma unroll
-		for (uint32_t c = 0; c < RXD_PER; ++c) {
-			if (c >= nc)
-				continue;
-			const uint32_t i = c * RXD_THREADS + t;
-			const uint32_t q = i < n ? s_q[i] : 0xFFu;
-			bool left = q < MI_CLS_DLV_GROUPS;
-			uint32_t rank = 0;
-			if (lane < MI_CLS_DLV_GROUPS)
-				s_gw[wave][lane] = 0u;
-			for (;;) {
-				const unsigned long long m = __ballot(left);
-				if (!m)
-					break;
-				const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)q, (int)__builtin_ctzll(m));
-				const unsigned long long mv = __ballot(left && q == v);
-				if (left && q == v) {
-					rank = (uint32_t)__popcll(mv & lt);
-					left = false;
-				}
-				if (lane == 0)
-					s_gw[wave][v] = (uint32_t)__popcll(mv);
+			for (uint32_t h = 0; h < RXD_SEG; ++h) {
+				const uint32_t i = (g0 + h) * WAVE + lane;
+				v[h] = i < n ? s_q[i] : 0xFFu;
 			}
-			__syncthreads();
-			if (q < MI_CLS_DLV_GROUPS) {
-				uint32_t before = 0;
-				for (uint32_t v = 0; v < wave; ++v)
-					before += s_gw[v][q];
-				pos[c] = s_gpos[q] + before + rank;
-			}
-			__syncthreads();
-			if (t < MI_CLS_DLV_GROUPS) {
-				uint32_t all = 0;
-				for (uint32_t v = 0; v < RXD_WAVES; ++v)
-					all += s_gw[v][t];
-				s_gpos[t] += all;
-			}
-			__syncthreads();
+#pragma unroll
+			for (uint32_t h = 0; h < RXD_SEG; ++h)
+#pragma unroll
+				for (uint32_t j = 0; j < 4; ++j)
+					cnt[j] += (uint32_t)__popcll(__ballot(v[h] == wave * 4u + j));
 		}
-	} else {
+		if (lane < 4u)
+			s_gcnt[wave * 4u + lane] = lane == 0 ? cnt[0] : lane == 1 ? cnt[1] : lane == 2 ? cnt[2] : cnt[3];
+		__syncthreads();
+		// group starts: every wave sums the counts before its own groups
+		uint32_t at[4];
+		{
+			const uint32_t v = s_gcnt[lane];
+			uint32_t below = 0;
+			for (uint32_t h = 0; h < MI_CLS_DLV_GROUPS; ++h)
+				below += h < wave * 4u ? (uint32_t)__builtin_amdgcn_readlane((int)v, (int)h) : 0u;
+			at[0] = below;
+			at[1] = at[0] + (uint32_t)__builtin_amdgcn_readlane((int)v, (int)(wave * 4u));
+			at[2] = at[1] + (uint32_t)__builtin_amdgcn_readlane((int)v, (int)(wave * 4u + 1u));
+			at[3] = at[2] + (uint32_t)__builtin_amdgcn_readlane((int)v, (int)(wave * 4u + 2u));
+			for (uint32_t h = 0; h < MI_CLS_DLV_GROUPS; ++h)
+				ngrp += (uint32_t)__builtin_amdgcn_readlane((int)v, (int)h);
+		}
+		for (uint32_t g0 = 0; g0 < nseg; g0 += RXD_SEG) {
+			uint32_t v[RXD_SEG];
+#pragma unroll
+			for (uint32_t h = 0; h < RXD_SEG; ++h) {
+				const uint32_t i = (g0 + h) * WAVE + lane;
+				v[h] = i < n ? s_q[i] : 0xFFu;
+			}
+#pragma unroll
+			for (uint32_t h = 0; h < RXD_SEG; ++h)
+#pragma unroll
+				for (uint32_t j = 0; j < 4; ++j) {
+					const bool mine = v[h] == wave * 4u + j;
+					const unsigned long long m = __ballot(mine);
+					if (mine)
+						s_perm[at[j] + (uint32_t)__popcll(m & lt)] =
+							(uint16_t)((g0 + h) * WAVE + lane);
+					at[j] += (uint32_t)__popcll(m);
+				}
+		}
 		__syncthreads();
 	}
 	// every output, after the last barrier
@@ -476,9 +480,9 @@ __global__ __launch_bounds__(RXD_THREADS) void mi_cls_rx_decide_kernel(mi_cls_rx
 		a.dec[i] = w[c];
 		d.dec[i] = w[c];
 		d.dq[i] = s_qh[qe[c]];
-		if (pos[c] != ~0u)
-			a.perm[pos[c]] = i;
 	}
+	for (uint32_t j = t; j < ngrp; j += RXD_THREADS)
+		a.perm[j] = s_perm[j];
 	if (group && t < MI_CLS_DLV_GROUPS)
 		a.gcnt[t] = s_gcnt[t];
 	if (t == 0) {
@@ -488,9 +492,9 @@ __global__ __launch_bounds__(RXD_THREADS) void mi_cls_rx_decide_kernel(mi_cls_rx
 		a.out->octets = s_ctr[3];
 		uint32_t sh = 0;
 		for (uint32_t k = 0; k < MI_CLS_RX_POOLS; ++k) {
-			a.out->used[k] = min(s_base[k], s_have[k]);
-			a.out->need[k] = s_base[k];
-			sh |= s_base[k] > s_have[k] ? 1u : 0u;
+			a.out->used[k] = min(s_need[k], s_have[k]);
+			a.out->need[k] = s_need[k];
+			sh |= s_need[k] > s_have[k] ? 1u : 0u;
 		}
 		a.out->short_pool = sh;
 	}
@@ -519,7 +523,7 @@ __global__ __launch_bounds__(DLV_THREADS) void mi_cls_rx_deliver_kernel(mi_cls_r
 	if (!e)
 		return;
 	uint8_t *meta = (uint8_t *)(uintptr_t)(e + a.meta_off);
-	const uint32_t len = a.slen[i];
+	const uint32_t len = d.dlen ? d.len[i] : a.slen[i];
 	if (sub < 4u) {
 		const mi_cls_result_t r = d.res[i];
 		const uint64_t dq = d.dq[i];
@@ -573,13 +577,13 @@ __global__ __launch_bounds__(DLV_THREADS) void mi_cls_rx_deliver_kernel(mi_cls_r
 // builds it for packets in page-locked pools.  A packet outside the
 // page-locked range gets an empty descriptor and sets not_in_place (the
 // host then stages and delivers the burst itself).
-__global__ __launch_bounds__(256) void mi_cls_rx_stage_kernel(mi_cls_rxc_args_t a, uint64_t bytes)
+__global__ __launch_bounds__(256) void mi_cls_rx_stage_kernel(mi_cls_rxc_args_t a, mi_cls_rxdev_t d, uint64_t bytes)
 {
 	// the page-locked flags go to LDS while the handles load (two host-link
 	// round trips per frame: the handle, then its header's words)
 	__shared__ uint8_t s_pin[64];
 	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-	const uint8_t pin = a.tab->rt_pinned[threadIdx.x & 63u];
+	const uint8_t pin = d.tab->rt_pinned[threadIdx.x & 63u];
 	const uint64_t hp = a.pk[min(i, a.n - 1u)];
 	s_pin[threadIdx.x & 63u] = pin;
 	__syncthreads();
@@ -589,17 +593,20 @@ __global__ __launch_bounds__(256) void mi_cls_rx_stage_kernel(mi_cls_rxc_args_t 
 	const uint64_t head = *(const uint64_t *)(h + a.head_off);
 	const uint32_t pool = *(const uint16_t *)(h + a.pool_off);
 	const mi_cls_pkt_meta_t *m = (const mi_cls_pkt_meta_t *)(h + a.meta_off);
-	const uint64_t d = head + m->data_off, base = (uint64_t)(uintptr_t)a.base;
+	const uint64_t da = head + m->data_off, base = (uint64_t)(uintptr_t)a.base;
 	const uint32_t l = min(m->len, 65535u);
-	const bool ok = pool < 64u && s_pin[pool] && d >= base && d - base + l + 16u <= bytes;
-	((uint32_t *)a.soff)[i] = ok ? (uint32_t)(d - base) : 0u;
+	const bool ok = pool < 64u && s_pin[pool] && da >= base && da - base + l + 16u <= bytes;
+	((uint32_t *)a.soff)[i] = ok ? (uint32_t)(da - base) : 0u;
 	((uint16_t *)a.slen)[i] = ok ? (uint16_t)l : (uint16_t)0;
 	((uint8_t *)a.ppool)[i] = (uint8_t)(pool + 1u);
+	d.len[i] = ok ? (uint16_t)l : (uint16_t)0;
+	d.pp[i] = (uint8_t)(pool + 1u);
 	if (!ok)
 		a.out->not_in_place = 1u;
 }
 
-int mi_cls_launch_rx_stage(hipStream_t st, const mi_cls_rxc_args_t &a, uint64_t bytes, bool preload)
+int mi_cls_launch_rx_stage(hipStream_t st, const mi_cls_rxc_args_t &a, const mi_cls_rxdev_t &d, uint64_t bytes,
+			   bool preload)
 {
 	if (preload) {
 		hipFuncAttributes fa;
@@ -607,14 +614,14 @@ int mi_cls_launch_rx_stage(hipStream_t st, const mi_cls_rxc_args_t &a, uint64_t 
 		       hipSuccess ? 0 : -EIO;
 	}
 	mi_cls_rxc_args_t h = a;
+	mi_cls_rxdev_t hd = d;
 	uint64_t b = bytes;
-	void *args[] = { &h, &b };
+	void *args[] = { &h, &hd, &b };
 	return hipLaunchKernel(reinterpret_cast<const void *>(&mi_cls_rx_stage_kernel),
 			       dim3((a.n + 255u) / 256u), dim3(256), args, 0, st) == hipSuccess ? 0 : -EIO;
 }
 
-int mi_cls_launch_rx_chain(hipStream_t cls, hipStream_t dlv, hipEvent_t dep, const mi_cls_rxc_args_t &a,
-			   const mi_cls_rxdev_t &d, bool preload)
+int mi_cls_launch_rx_chain(hipStream_t st, const mi_cls_rxc_args_t &a, const mi_cls_rxdev_t &d, bool preload)
 {
 	if (preload) {
 		hipFuncAttributes fa;
@@ -627,10 +634,9 @@ int mi_cls_launch_rx_chain(hipStream_t cls, hipStream_t dlv, hipEvent_t dep, con
 	mi_cls_rxdev_t hd = d;
 	void *args[] = { &h, &hd };
 	if (hipLaunchKernel(reinterpret_cast<const void *>(&mi_cls_rx_decide_kernel), dim3(1),
-			    dim3(RXD_THREADS), args, 0, cls) != hipSuccess ||
-	    hipEventRecord(dep, cls) != hipSuccess || hipStreamWaitEvent(dlv, dep, 0) != hipSuccess)
+			    dim3(RXD_THREADS), args, 0, st) != hipSuccess)
 		return -EIO;
 	const unsigned grid = (a.n + DLV_PER_BLOCK - 1u) / DLV_PER_BLOCK;
 	return hipLaunchKernel(reinterpret_cast<const void *>(&mi_cls_rx_deliver_kernel), dim3(grid),
-			       dim3(DLV_THREADS), args, 0, dlv) == hipSuccess ? 0 : -EIO;
+			       dim3(DLV_THREADS), args, 0, st) == hipSuccess ? 0 : -EIO;
 }

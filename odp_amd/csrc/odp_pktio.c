@@ -62,7 +62,7 @@ enum { ST_OPENED = 0, ST_STARTED, ST_STOPPED };
 /* receive pipeline depth (pktio_recv): classifications and GPU deliveries
  * in flight */
 #define RX_CLS_DEPTH 1
-#define RX_DLV_DEPTH 2
+#define RX_DLV_DEPTH 3
 #define RX_SETS (1 + RX_CLS_DEPTH + RX_DLV_DEPTH)
 /* in-place loop bursts: offsets from the pinned arena's base stay below the
  * kernel's out-of-range offset */
@@ -2507,6 +2507,12 @@ static int rxc_table(rt_pktio_t *e)
 		memset(e->rx_want, 0, sizeof(e->rx_want));   /* first bursts: as many as frames */
 	e->rx_np = np;
 	e->rxtab_gen = tg;
+	{
+		/* a new stamp per rewrite: the device's copies follow it */
+		static uint64_t stamps;
+
+		e->rxtab->stamp = __atomic_add_fetch(&stamps, 1, __ATOMIC_RELAXED);
+	}
 	e->rxtab_ok = ok && tg == g;
 	return e->rxtab_ok ? 0 : -1;
 }
