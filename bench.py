@@ -320,9 +320,10 @@ def time_runtime(batch, prog, n_frames=200_000, loops=10):
                 out[mode].update(in_packets=v[0], in_errors=v[1], in_discards=v[2])
     out["note"] = (f"ODP runtime receive path, steady state after odp_pktio_start ({n} "
                    f"frames x {loops} loops of this workload's traffic; 4096-frame bursts "
-                   f"pipelined (classification of one burst, two GPU deliveries in flight); "
-                   f"packet metadata, frame copies and the group-by-queue "
-                   f"done by the GPU delivery kernel into page-locked pools; CoS enqueue; one "
+                   f"pipelined, each a receive chain on the GPU (classify, decide, deliver; "
+                   f"four bursts in flight on two streams): per-frame fates, packets and "
+                   f"queue groups decided, packet metadata and frame copies written into "
+                   f"page-locked pools by the GPU; CoS enqueue; one "
                    f"application thread draining the queues): a pcap pktio whose page-locked "
                    f"frame store the GPU reads in place through odp_pktin_recv (direct) and "
                    f"odp_schedule (sched), and the loop pktio (loop_direct: rounds of 32768 "
