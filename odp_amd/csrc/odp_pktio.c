@@ -173,7 +173,8 @@ typedef struct {
 				 * then of delivering: ns preparing / enqueueing, TSC ticks in
 				 * packet allocation / frame copies; GPU delivery: ns deciding +
 				 * taking packets + entries, ns in the delivery kernel (submit to
-				 * wait), ns enqueueing, bursts */
+				 * wait), ns enqueueing, bursts; receive chain: ns in its
+				 * submit call (odp_amd_cls_rx_chain) */
 } rt_pktio_t;
 
 static void rx_sets_free(rt_pktio_t *e);
@@ -861,7 +862,7 @@ int odp_pktio_close(odp_pktio_t h)
 			" deliver_ns %" PRIu64 " (prepare_ns %" PRIu64 " enqueue_ns %" PRIu64
 			" alloc_tsc %" PRIu64 " copy_tsc %" PRIu64 ") gpu_bursts %" PRIu64
 			" (decide_ns %" PRIu64 " submit_ns %" PRIu64 " kernel_ns %" PRIu64 " enqueue_ns %" PRIu64
-			") cls_submit_ns %" PRIu64 "\n", e->name,
+			") chain_submit_ns %" PRIu64 "\n", e->name,
 			e->prof[3], e->prof[0], e->prof[1], e->prof[2], e->prof[4], e->prof[5], e->prof[6],
 			e->prof[7], e->prof[11], e->prof[8], e->prof[12], e->prof[9], e->prof[10], e->prof[13]);
 	if (e->inq != ODP_QUEUE_INVALID) {
@@ -2618,7 +2619,11 @@ static int rxc_submit(rt_pktio_t *e, rx_set_t *s)
 	s->gen = odp_amd_cls_generation();
 	s->dgen = e->rxtab_gen;
 	s->dticket = 0;
-	if (odp_amd_cls_rx_chain(e->hdl, s->base, s->bytes, &a, &s->dticket) != 0) {
+	const uint64_t tc = prof_ns();
+	const int crc = odp_amd_cls_rx_chain(e->hdl, s->base, s->bytes, &a, &s->dticket);
+
+	e->prof[13] += prof_ns() - tc;
+	if (crc != 0) {
 		for (uint32_t k = 0; k < s->cnp; k++)
 			rt_packet_return_raw(s->cpool[k], (const odp_packet_t *)(const void *)(s->got + s->cbase[k]),
 					     (int)s->chave[k]);
