@@ -428,7 +428,7 @@ def _bench_cfg(cls, cfg, a, dev, local, steps, warmup, pktin_opt, parity, full_b
     if pktin_opt:
         c2.set_pktin_opt(pktin_opt)
     log("  rules loaded, waiting for the specialised kernel")
-    spec = c2.spec_wait() == 0 and not pktin_opt
+    spec = c2.spec_wait() == 0
     info = c2.program_info()
     engine = ("linear scan" if info["blocks"] == 0 else
               ["direct", "candidate lists", "bitmap", "wide bitmap", "single candidate"][

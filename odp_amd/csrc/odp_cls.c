@@ -1038,10 +1038,12 @@ int odp_amd_cls_classify(odp_pktio_t h, const uint8_t *pkts_dev, const uint32_t 
 	rc = ensure_ctx(e);
 	if (rc)
 		return rc;
+	/* the options before the rules: a program load specialises the kernel
+	 * of the options in force (the option kernel when they are on) */
+	mi_cls_pktin_opt_set(e->ctx, e->pktin_opt);
 	rc = sync_rules(e, stream);
 	if (rc)
 		return rc;
-	mi_cls_pktin_opt_set(e->ctx, e->pktin_opt);
 	return mi_cls_classify(e->ctx, pkts_dev, off_dev, len_dev, n, (mi_cls_result_t *)out_dev,
 			       stream);
 }
@@ -1363,10 +1365,10 @@ int odp_amd_cls_rx_chain(odp_pktio_t h, const uint8_t *pkts, size_t bytes,
 	rc = ensure_ctx(e);
 	if (rc)
 		return rc;
+	mi_cls_pktin_opt_set(e->ctx, e->pktin_opt);
 	rc = sync_rules(e, NULL);
 	if (rc)
 		return rc;
-	mi_cls_pktin_opt_set(e->ctx, e->pktin_opt);
 	return mi_cls_rx_chain_submit(e->ctx, pkts, bytes, args, ticket);
 }
 
@@ -1484,6 +1486,8 @@ int odp_amd_cls_classify_host(odp_pktio_t h, const uint8_t *pkts, size_t bytes,
 	rc = ensure_ctx(e);
 	if (rc)
 		return rc;
+	if (!e->grp)
+		mi_cls_pktin_opt_set(e->ctx, e->pktin_opt);
 	rc = sync_rules(e, NULL);
 	if (rc)
 		return rc;
@@ -1509,6 +1513,8 @@ int odp_amd_cls_classify_host_submit(odp_pktio_t h, const uint8_t *pkts, size_t 
 	rc = ensure_ctx(e);
 	if (rc)
 		return rc;
+	if (!e->grp)
+		mi_cls_pktin_opt_set(e->ctx, e->pktin_opt);
 	rc = sync_rules(e, NULL);
 	if (rc)
 		return rc;
@@ -1584,6 +1590,8 @@ int odp_amd_cls_spec_wait(odp_pktio_t h)
 	rc = ensure_ctx(e);
 	if (rc)
 		return rc;
+	if (!e->grp)
+		mi_cls_pktin_opt_set(e->ctx, e->pktin_opt);   /* the options' kernel */
 	rc = sync_rules(e, NULL);
 	if (rc)
 		return rc;

@@ -173,3 +173,36 @@ def test_sctp_crc_every_piece_split(built, gpu, ipver):
     got = both([R.cos("d", queue=1), ("default", 0)], b, CK.SCTP_CK, f"sctp splits ipv{ipver}")
     assert ((got["in_flags"] >> 31) & 1).all()
     assert np.array_equal((got["err"] & CK.E_L4CK) != 0, bad)
+
+
+@pytest.mark.parametrize("name", ["all_ck", "all_ck_drop", "ipv4_ck", "sctp_tcp_ck"])
+@pytest.mark.parametrize("cfg", [3, 2])
+def test_specialised_option_kernel(built, gpu, name, cfg):
+    """With pktin options on, a flat program gets the option kernel with its
+    block compiled in (spec_setup: the checksum instantiation): the same
+    records as the oracle on the zoo, the checksum frames and the config's
+    own traffic; turning the options off again specialises the plain kernel."""
+    from odp_amd.cls import Classifier
+    b0, prog = R.CONFIGS[cfg](3000)
+    pg.set_checksums(b0)
+    frames = [b0.frame(i) for i in range(b0.n)] + _frames(5)
+    b = pg.batch_from_frames(frames)
+    exp, _ = oracle_run(prog, b, pktin_opt=OPTS[name])
+    c = Classifier(gpu=0)
+    try:
+        c.apply(prog)
+        c.set_pktin_opt(OPTS[name])
+        assert c.spec_wait() == 0
+        got = c.classify(b)
+        ll = c.last_launch()
+        assert ll["ck"] and ll["specialised"], ll
+        assert_same(got, exp, b, f"config {cfg} {name} (specialised option kernel)")
+        c.set_pktin_opt(0)
+        assert c.spec_wait() == 0
+        got0 = c.classify(b)
+        ll = c.last_launch()
+        assert not ll["ck"] and ll["specialised"], ll
+        exp0, _ = oracle_run(prog, b)
+        assert_same(got0, exp0, b, f"config {cfg} options off")
+    finally:
+        c.close()
